@@ -1,0 +1,199 @@
+"""Throughput benchmark of the vectorised Futbol env step on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs B] [--players 2] [--kind v1|v0]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N
+
+Workload (BASELINE.json configs[1]/[3]): B = 65 536 independent 2v2 envs_v1
+matches per GPU, synthetic random left-team actions (Philox, generated on the
+GPU by fill_actions), opponent random actions drawn inside the step kernel,
+DummyVecEnv auto-reset; every step writes obs/reward/done to HBM.  A "step" =
+fill_actions + one env-step launch over all B envs.  N > 1: one process per
+GPU, env shards with global env ids rank*B..; weak scaling; one RCCL
+all_reduce(SUM) of [episode-return sum, episodes, env-steps] every 300 steps
+(the only collective: the envs never exchange anything).
+
+Prints ONE JSON line (rank 0).  `roofline` is the step kernel's algorithmic
+HBM bytes (579 B per 2v2 env-step) / its average duration,
+measured live with HIP events on the launch stream; `cpu_baseline` times the
+oracle/ C restatement of the same step on the host (kind "port": the
+reference's own v1 step needs pymunk, absent here).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "gym-futbol_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "env-steps/sec (whole node), 2v2 Futbol, batch=65536 envs, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
+
+
+def algo_bytes_per_env_step(kind, n, out_bytes):
+    """state read+write + actions + obs/reward/done writes (contact cache excluded)."""
+    if kind == "v1":
+        nb = 2 * n + 1
+        return 2 * (48 * nb + 5) + 2 * n + 4 * nb * out_bytes + out_bytes + 1
+    return 2 * (25 * 8 + 14) + 1 + 30 * out_bytes + out_bytes + 1
+
+
+def cpu_baseline(kind, n, budget_s=12.0, B=65536):
+    """Oracle (faithful build, 1 thread) on a bounded sample of the same workload."""
+    from oracle import oracle as O
+    if kind == "v1":
+        ora = O.V1Vec(B, N=n, seed=0)
+        nact, adim = 5, 2 * n
+    else:
+        ora = O.V0Vec(B, seed=0, random_opp=False)
+        nact, adim = 16, 1
+    ora.reset()
+    rng = np.random.default_rng(1234)
+    steps = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        a = rng.integers(0, nact, (B, adim)).astype(np.int32)
+        ora.step(a if kind == "v1" else a.reshape(-1), nthreads=1)
+        steps += 1
+    dt = time.perf_counter() - t0
+    return {"value": steps * B / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": "oracle/liboracle.so (C restatement of the %s step), 1 thread, %d envs x %d steps (%.1f s)"
+                      % ("envs_v1 2v2" if kind == "v1" else "v0 hard-coded-opponent", B, steps, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3000)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--players", type=int, default=2)
+    ap.add_argument("--kind", default="v1", choices=["v1", "v0"])
+    ap.add_argument("--graph", type=int, default=1, help="replay the timed steps from a hipGraph")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-steps", type=int, default=200, help="steps timed per-kernel with HIP events")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    from gym_futbol_amd import FutbolVecEnv
+    B = args.envs
+    n = args.players
+    kw = {"number_of_player": n} if args.kind == "v1" else {"random_opp": False}
+    venv = FutbolVecEnv(args.kind, B, device=dev, seed=0, env_id_base=rank * B, dtype=torch.float32, **kw)
+    venv.reset()
+    act = venv._act
+    stream = torch.cuda.current_stream(dev)
+    ALL = 2**64 - 1  # device step counter (advanced by every step launch)
+
+    def one_step():
+        venv.random_actions(ALL, seed=1234, out=act)
+        venv.step_raw(act)
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize(dev)
+
+    # per-kernel timing of the dominant kernel (the env step) with HIP events on its stream
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.profile_steps)]
+    for e0, e1 in ev:
+        venv.random_actions(ALL, seed=1234, out=act)
+        e0.record(stream)
+        venv.step_raw(act)
+        e1.record(stream)
+    torch.cuda.synchronize(dev)
+    kernel_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ev]))
+
+    graph = None
+    G = 100
+    if args.graph:
+        graph = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(stream)
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(graph, stream=s):
+                for _ in range(G):
+                    one_step()
+        stream.wait_stream(s)
+        torch.cuda.synchronize(dev)
+
+    stats_buf = torch.zeros(3, dtype=torch.float64, device=dev)
+    venv.episode_stats(clear=True)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    done_steps = 0
+    while done_steps < args.steps:
+        chunk = min(G, args.steps - done_steps) if graph is not None else 1
+        if graph is not None and chunk == G:
+            graph.replay()
+        else:
+            for _ in range(chunk):
+                one_step()
+        prev = done_steps
+        done_steps += chunk
+        if dist is not None and done_steps // 300 != prev // 300:
+            stats_buf.copy_(venv.episode_stats(clear=False))
+            dist.all_reduce(stats_buf)  # RCCL over xGMI: [sum return, episodes, env-steps]
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    stats = venv.episode_stats(clear=False).cpu().numpy()
+    if dist is not None:
+        st = torch.as_tensor(stats, device=dev)
+        dist.all_reduce(st)
+        stats = st.cpu().numpy()
+
+    total_env_steps = B * args.steps * world
+    value = total_env_steps / elapsed
+    out_bytes = 4
+    per_env = algo_bytes_per_env_step(args.kind, n, out_bytes)
+    achieved = per_env * B / (kernel_ms * 1e-3) / 1e9
+    line = {
+        "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": ("C2/C4: %d envs/GPU envs_v1 %dv%d, synthetic random actions, auto-reset"
+                                % (B, n, n)) if args.kind == "v1" else
+                   ("C3: %d envs/GPU v0 FutbolEnv, hard-coded opponent" % B),
+                   "envs_per_gpu": B, "global_envs": B * world, "parallelism": "dp%d" % world,
+                   "obs_dtype": "f32", "hip_graph": bool(graph is not None)},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "v1_step_kernel<%d,float>" % n if args.kind == "v1" else "v0_step_kernel<float>",
+                     "kernel_ms": kernel_ms, "algo_bytes_per_env_step": per_env},
+        "episodes": {"finished": float(stats[1]),
+                     "mean_return": float(stats[0] / stats[1]) if stats[1] else None},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args.kind, n)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    venv.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,74 @@
+"""Build the MI355X (gfx950) kernels + C ABI into gym_futbol_amd/libfutbol_amd.so.
+
+    python gym-futbol_amd/build.py [--force] [-j N]
+
+Each csrc/*.hip translation unit is compiled by hipcc in parallel (one TU per
+team size for the envs_v1 kernels), then linked into one shared library that
+exports exactly the C ABI of include/futbol.h.  -ffp-contract=off: the env
+math must round exactly like the reference's (no FMA contraction).
+"""
+import argparse
+import glob
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+OBJ = os.path.join(HERE, "build", "obj")
+LIB = os.path.join(HERE, "gym_futbol_amd", "libfutbol_amd.so")
+ARCH = os.environ.get("FUTBOL_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CFLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fPIC",
+          "-Wall", "-Wno-unused-function", "-I" + os.path.join(ROOT, "include")]
+
+
+def _deps():
+    return glob.glob(os.path.join(CSRC, "*.hpp")) + [os.path.join(ROOT, "include", "futbol.h"), __file__]
+
+
+def _stale(target, sources):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(s) > t for s in sources)
+
+
+def _compile(src, force):
+    obj = os.path.join(OBJ, os.path.basename(src) + ".o")
+    if force or _stale(obj, [src] + _deps()):
+        cmd = [HIPCC] + CFLAGS + ["-c", src, "-o", obj]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("hipcc failed for %s:\n%s\n%s" % (src, " ".join(cmd), r.stderr[-8000:]))
+    return obj
+
+
+def build(force=False, jobs=None, verbose=True):
+    os.makedirs(OBJ, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, force), srcs))
+    if force or _stale(LIB, objs):
+        cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("link failed:\n%s" % r.stderr[-8000:])
+        if verbose:
+            print("built", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", type=int, default=None)
+    a = ap.parse_args()
+    try:
+        build(a.force, a.j)
+    except RuntimeError as e:
+        print(e, file=sys.stderr)
+        sys.exit(1)

@@ -1,0 +1,489 @@
+// futbol_capi.hip -- the C ABI of include/futbol.h: context lifetime, the HBM
+// state allocation, constants derived from the reference's constructor
+// kwargs, and stream-ordered launches.  No host<->device sync on the
+// step/reset path (graph-capturable); no torch types.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+#include <string>
+#include <vector>
+#include "../../include/futbol.h"
+#include "futbol_kernels.hpp"
+#include "futbol_rng.hpp"
+
+using namespace futbol;
+
+namespace {
+
+struct Field {
+    const char* name;
+    size_t offset;
+    int32_t type;  // 0 f64, 1 u64, 2 u32, 3 u16, 4 u8
+    int64_t count;
+};
+
+size_t type_size(int t) { return t == 0 || t == 1 ? 8 : (t == 2 ? 4 : (t == 3 ? 2 : 1)); }
+
+thread_local std::string g_create_error;
+
+}  // namespace
+
+struct FutbolCtx {
+    FutbolConfig cfg;
+    int device = 0;
+    uint64_t seed = 0, env_base = 0;
+    int B = 0, N = 0, obs_dim = 0, act_dim = 0, K_done = 0;
+    void* d_params = nullptr;
+    char* d_state = nullptr;
+    size_t state_bytes = 0;
+    std::vector<Field> fields;
+    double* d_spill = nullptr;
+    unsigned long long* d_invalid = nullptr;  // [0] invalid-action count, [1] synthetic-policy step
+    V1Ptrs v1{};
+    V0Ptrs v0{};
+    double steps_since_clear = 0.0;
+    std::string err;
+};
+
+#define FB_CHECK_HIP(ctx, expr)                                                                         \
+    do {                                                                                                \
+        hipError_t _e = (expr);                                                                         \
+        if (_e != hipSuccess) {                                                                         \
+            (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(_e);                             \
+            return FUTBOL_EHIP;                                                                         \
+        }                                                                                               \
+    } while (0)
+
+static int fail(FutbolCtx* ctx, int code, const std::string& msg)
+{
+    if (ctx) ctx->err = msg;
+    else g_create_error = msg;
+    return code;
+}
+
+extern "C" int futbol_config_default(int32_t env_kind, int32_t number_of_player, FutbolConfig* c)
+{
+    if (!c) return FUTBOL_EINVAL;
+    memset(c, 0, sizeof(*c));
+    c->abi_version = FUTBOL_ABI_VERSION;
+    c->env_kind = env_kind;
+    c->out_dtype = FUTBOL_F32;
+    // envs_v1/futbol_env.py:19-28,63-65
+    c->number_of_player = number_of_player > 0 ? number_of_player : 5;
+    c->width = 105;
+    c->height = 68;
+    c->total_time = 30;
+    // envs/futbol_env.py:18-58,134-138
+    c->length0 = 105;
+    c->width0 = 68;
+    c->goal_size0 = 10;
+    c->game_time0 = 40;
+    c->player_speed0 = 12;
+    c->shoot_speed0 = 20;
+    c->one_goal_end0 = 0;
+    c->action_as_int0 = 1;
+    c->only_reward_goal0 = 0;
+    c->random_opp0 = 1;
+    c->auto_reset = 1;
+    return (env_kind == FUTBOL_ENV_V0 || env_kind == FUTBOL_ENV_V1) ? FUTBOL_OK : FUTBOL_EINVAL;
+}
+
+// Team._create_pos_array (team.py:52-112), player k of a team
+static void formation(int N, double W, double H, int side, int k, double* x, double* y)
+{
+    if (N <= 3) {
+        *x = side == 0 ? W * 0.25 : W * 0.75;
+        *y = (H / (double)(N + 1)) * (double)(k + 1);
+    } else if (N <= 6) {
+        if (k < 3) { *x = side == 0 ? (W * 1) / 6 : (W * 5) / 6; *y = (H / 4.0) * (double)(k + 1); }
+        else { *x = side == 0 ? (W * 2) / 6 : (W * 4) / 6; *y = (H / (double)(N - 3 + 1)) * (double)(k - 3 + 1); }
+    } else {
+        if (k < 4) { *x = side == 0 ? (W * 1) / 8 : (W * 7) / 8; *y = (H / 5.0) * (double)(k + 1); }
+        else if (k < 7) { *x = side == 0 ? (W * 2) / 8 : (W * 6) / 8; *y = (H / 4.0) * (double)(k - 4 + 1); }
+        else { *x = side == 0 ? (W * 3) / 8 : (W * 5) / 8; *y = (H / (double)(N - 7 + 1)) * (double)(k - 7 + 1); }
+    }
+}
+
+static void fill_v1_params(const FutbolConfig* c, uint64_t seed, uint64_t env_base, int B, int K_done, V1Params* p)
+{
+    memset(p, 0, sizeof(*p));
+    const double W = c->width, H = c->height, G = 20.0;  // GOAL_SIZE (envs_v1/futbol_env.py:21)
+    p->W = W;
+    p->H = H;
+    const double lo = H / 2 - G / 2, hi = H / 2 + G / 2;
+    // _setup_walls (envs_v1/futbol_env.py:182-234): 6 walls then 6 goal-box segments
+    const double seg[12][4] = {{0, 0, 0, lo},       {0, hi, 0, H},          {0, H, W, H},
+                               {W, 0, W, lo},       {W, hi, W, H},          {0, 0, W, 0},
+                               {-2, lo, -2, hi},    {-2, lo, 0, lo},        {-2, hi, 0, hi},
+                               {W + 2, lo, W + 2, hi}, {W, lo, W + 2, lo}, {W, hi, W + 2, hi}};
+    for (int s = 0; s < 12; ++s) {
+        p->sax[s] = seg[s][0];
+        p->say[s] = seg[s][1];
+        p->sbx[s] = seg[s][2];
+        p->sby[s] = seg[s][3];
+        // cpSegmentShapeCacheData: bb = (min - r, ..., max + r), r = 1
+        const double l = seg[s][0] < seg[s][2] ? seg[s][0] : seg[s][2];
+        const double r = seg[s][0] < seg[s][2] ? seg[s][2] : seg[s][0];
+        const double b = seg[s][1] < seg[s][3] ? seg[s][1] : seg[s][3];
+        const double t = seg[s][1] < seg[s][3] ? seg[s][3] : seg[s][1];
+        p->sl[s] = l - 1.0;
+        p->sb[s] = b - 1.0;
+        p->sr[s] = r + 1.0;
+        p->st[s] = t + 1.0;
+    }
+    const int N = c->number_of_player;
+    for (int side = 0; side < 2; ++side)
+        for (int k = 0; k < N; ++k) formation(N, W, H, side, k, &p->fx[side * N + k], &p->fy[side * N + k]);
+    p->fx[2 * N] = W * 0.5;  // Ball(width*0.5, height*0.5) (envs_v1/futbol_env.py:122,135)
+    p->fy[2 * N] = H * 0.5;
+    // cpSpace defaults (Chipmunk 7 cpSpaceInit): collisionSlop 0.1f, collisionBias cpfpow(1.0f - 0.1f, 60.0f);
+    // damping 0.95 (envs_v1/futbol_env.py:99); dt 0.1 (TIME_STEP) and 1e-4 (_position_to_initial)
+    const double cbias = pow((double)(1.0f - 0.1f), 60.0);
+    p->dtv[0] = 0.0;
+    p->dtv[1] = 0.0001;
+    p->dtv[2] = 0.1;
+    for (int i = 1; i < 3; ++i) {
+        p->damp[i] = pow(0.95, p->dtv[i]);
+        p->biasc[i] = 1.0 - pow(cbias, p->dtv[i]);
+    }
+    p->slop = (double)0.1f;
+    p->seed = seed;
+    p->env_base = (uint32_t)env_base;
+    p->B = B;
+    p->K_done = K_done;
+    p->auto_reset = c->auto_reset;
+}
+
+// steps until `current_time += 0.1` (fp64, from 0) makes `current_time > total` (v1, :478-481)
+static int v1_episode_steps(double total)
+{
+    double t = 0.0;
+    for (int k = 1; k <= kMaxSteps; ++k) {
+        t += 0.1;
+        if (t > total) return k;
+    }
+    return -1;
+}
+
+// v0 checks `time >= game_time` BEFORE `time += 0.1` (envs/futbol_env.py:712-716)
+static int v0_episode_steps(double game_time)
+{
+    double t = 0.0;
+    for (int k = 1; k <= kMaxSteps; ++k) {
+        if (t >= game_time) return k;
+        t += 0.1;
+    }
+    return -1;
+}
+
+static void fill_v0_params(const FutbolConfig* c, uint64_t seed, uint64_t env_base, int B, int K_done, V0Params* p)
+{
+    memset(p, 0, sizeof(*p));
+    p->length = c->length0;
+    p->width = c->width0;
+    p->goal_size = c->goal_size0;
+    p->player_speed = c->player_speed0;
+    p->shoot_speed = c->shoot_speed0;
+    // random.randint(goal_down + 3, goal_up - 3) (envs/futbol_env.py:305-306)
+    p->ty_lo = (int)(c->width0 / 2 - c->goal_size0 / 2 + 3);
+    p->ty_hi = (int)(c->width0 / 2 + c->goal_size0 / 2 - 3);
+    // random.randint(shoot_speed - 16, shoot_speed) (:367)
+    p->shoot_lo = (int)c->shoot_speed0 - 16;
+    p->shoot_hi = (int)c->shoot_speed0;
+    p->one_goal_end = c->one_goal_end0;
+    p->only_reward_goal = c->only_reward_goal0;
+    p->random_opp = c->random_opp0;
+    p->action_as_int = c->action_as_int0;
+    p->seed = seed;
+    p->env_base = (uint32_t)env_base;
+    p->B = B;
+    p->K_done = K_done;
+    p->auto_reset = c->auto_reset;
+}
+
+static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+extern "C" int futbol_create(const FutbolConfig* cfg, int32_t device, uint64_t seed, uint64_t env_id_base,
+                             int32_t num_envs, FutbolCtx** out)
+{
+    if (!cfg || !out) return fail(nullptr, FUTBOL_EINVAL, "null argument");
+    *out = nullptr;
+    if (cfg->abi_version != FUTBOL_ABI_VERSION) return fail(nullptr, FUTBOL_EINVAL, "ABI version mismatch");
+    if (num_envs <= 0) return fail(nullptr, FUTBOL_EINVAL, "num_envs must be > 0");
+    if (env_id_base + (uint64_t)num_envs > 0xffffffffull)
+        return fail(nullptr, FUTBOL_EINVAL, "global env ids must fit in 32 bits");
+    if (cfg->out_dtype != FUTBOL_F32 && cfg->out_dtype != FUTBOL_F64) return fail(nullptr, FUTBOL_EINVAL, "out_dtype");
+    if (cfg->env_kind == FUTBOL_ENV_V1 && !v1_supported(cfg->number_of_player))
+        return fail(nullptr, FUTBOL_EUNSUPPORTED, "number_of_player must be one of 1,2,3,5,10");
+    if (cfg->env_kind != FUTBOL_ENV_V1 && cfg->env_kind != FUTBOL_ENV_V0)
+        return fail(nullptr, FUTBOL_EINVAL, "env_kind");
+
+    FutbolCtx* ctx = new FutbolCtx();
+    ctx->cfg = *cfg;
+    ctx->device = device;
+    ctx->seed = seed;
+    ctx->env_base = env_id_base;
+    ctx->B = num_envs;
+    const int B = num_envs;
+    hipError_t he = hipSetDevice(device);
+    if (he != hipSuccess) {
+        delete ctx;
+        return fail(nullptr, FUTBOL_EHIP, std::string("hipSetDevice: ") + hipGetErrorString(he));
+    }
+
+    size_t off = 0;
+    auto add = [&](const char* name, int type, int64_t count) {
+        ctx->fields.push_back({name, off, type, count});
+        off = align_up(off + type_size(type) * (size_t)count);
+    };
+    if (cfg->env_kind == FUTBOL_ENV_V1) {
+        const int N = cfg->number_of_player, Nb = 2 * N + 1, P = v1_npairs(N);
+        ctx->N = N;
+        ctx->obs_dim = 4 * Nb;
+        ctx->act_dim = 2 * N;
+        ctx->K_done = v1_episode_steps(cfg->total_time);
+        if (ctx->K_done < 0) {
+            delete ctx;
+            return fail(nullptr, FUTBOL_EUNSUPPORTED, "total_time too long for the 14-bit step counter");
+        }
+        for (const char* f : {"px", "py", "vx", "vy", "bx", "by"}) add(f, 0, (int64_t)Nb * B);
+        add("meta", 1, B);
+        add("ep_ret", 0, B);
+        add("ckey", 3, (int64_t)P * B);
+        add("cjn", 0, (int64_t)P * B);
+        add("stat_ret", 0, B);
+        add("stat_cnt", 2, B);
+    } else {
+        ctx->N = 2;
+        ctx->obs_dim = 30;
+        ctx->act_dim = cfg->action_as_int0 ? 1 : 2;
+        ctx->K_done = v0_episode_steps(cfg->game_time0);
+        if (ctx->K_done < 0) {
+            delete ctx;
+            return fail(nullptr, FUTBOL_EUNSUPPORTED, "game_time too long for the 14-bit step counter");
+        }
+        add("row", 0, (int64_t)25 * B);
+        add("view", 0, (int64_t)8 * B);
+        add("meta", 1, B);
+        add("ep_ret", 0, B);
+        add("score", 2, (int64_t)2 * B);
+        add("stat_ret", 0, B);
+        add("stat_cnt", 2, B);
+    }
+    ctx->state_bytes = off;
+    auto bail = [&](hipError_t e, const char* what) {
+        std::string m = std::string(what) + ": " + hipGetErrorString(e);
+        futbol_destroy(ctx);
+        return fail(nullptr, FUTBOL_ENOMEM, m);
+    };
+    if ((he = hipMalloc((void**)&ctx->d_state, ctx->state_bytes)) != hipSuccess) return bail(he, "hipMalloc(state)");
+    if ((he = hipMemset(ctx->d_state, 0, ctx->state_bytes)) != hipSuccess) return bail(he, "hipMemset(state)");
+    if ((he = hipMalloc((void**)&ctx->d_invalid, 2 * sizeof(unsigned long long))) != hipSuccess)
+        return bail(he, "hipMalloc(counters)");
+    if ((he = hipMemset(ctx->d_invalid, 0, 2 * sizeof(unsigned long long))) != hipSuccess)
+        return bail(he, "hipMemset");
+
+    auto fptr = [&](const char* name) -> char* {
+        for (auto& f : ctx->fields)
+            if (!strcmp(f.name, name)) return ctx->d_state + f.offset;
+        return nullptr;
+    };
+    if (cfg->env_kind == FUTBOL_ENV_V1) {
+        const int N = ctx->N;
+        const size_t slots = v1_spill_slots(N);
+        if ((he = hipMalloc((void**)&ctx->d_spill, slots * 8 * sizeof(double) * (size_t)B)) != hipSuccess)
+            return bail(he, "hipMalloc(spill)");
+        V1Params hp;
+        fill_v1_params(cfg, seed, env_id_base, B, ctx->K_done, &hp);
+        if ((he = hipMalloc(&ctx->d_params, sizeof(V1Params))) != hipSuccess) return bail(he, "hipMalloc(params)");
+        if ((he = hipMemcpy(ctx->d_params, &hp, sizeof(hp), hipMemcpyHostToDevice)) != hipSuccess)
+            return bail(he, "hipMemcpy(params)");
+        V1Ptrs& s = ctx->v1;
+        s.px = (double*)fptr("px");
+        s.py = (double*)fptr("py");
+        s.vx = (double*)fptr("vx");
+        s.vy = (double*)fptr("vy");
+        s.bx = (double*)fptr("bx");
+        s.by = (double*)fptr("by");
+        s.meta = (uint64_t*)fptr("meta");
+        s.ep_ret = (double*)fptr("ep_ret");
+        s.ckey = (uint16_t*)fptr("ckey");
+        s.cjn = (double*)fptr("cjn");
+        s.stat_ret = (double*)fptr("stat_ret");
+        s.stat_cnt = (uint32_t*)fptr("stat_cnt");
+        s.spill = ctx->d_spill;
+        s.invalid = ctx->d_invalid;
+        s.act_step = ctx->d_invalid + 1;
+        int rc = launch_v1(N, (const V1Params*)ctx->d_params, B, s, 0, 1, nullptr, nullptr, nullptr, nullptr,
+                           nullptr, nullptr, 1, 0);
+        if (rc) return bail(hipGetLastError(), "launch(init)");
+    } else {
+        V0Params hp;
+        fill_v0_params(cfg, seed, env_id_base, B, ctx->K_done, &hp);
+        if ((he = hipMalloc(&ctx->d_params, sizeof(V0Params))) != hipSuccess) return bail(he, "hipMalloc(params)");
+        if ((he = hipMemcpy(ctx->d_params, &hp, sizeof(hp), hipMemcpyHostToDevice)) != hipSuccess)
+            return bail(he, "hipMemcpy(params)");
+        V0Ptrs& s = ctx->v0;
+        s.row = (double*)fptr("row");
+        s.view = (double*)fptr("view");
+        s.meta = (uint64_t*)fptr("meta");
+        s.ep_ret = (double*)fptr("ep_ret");
+        s.score = (uint32_t*)fptr("score");
+        s.stat_ret = (double*)fptr("stat_ret");
+        s.stat_cnt = (uint32_t*)fptr("stat_cnt");
+        s.invalid = ctx->d_invalid;
+        s.act_step = ctx->d_invalid + 1;
+        int rc = launch_v0((const V0Params*)ctx->d_params, B, s, 0, 1, nullptr, nullptr, nullptr, nullptr, nullptr,
+                           nullptr, 1, 0);
+        if (rc) return bail(hipGetLastError(), "launch(init)");
+    }
+    if ((he = hipDeviceSynchronize()) != hipSuccess) return bail(he, "init kernel");
+    *out = ctx;
+    return FUTBOL_OK;
+}
+
+extern "C" int futbol_destroy(FutbolCtx* ctx)
+{
+    if (!ctx) return FUTBOL_OK;
+    hipSetDevice(ctx->device);
+    if (ctx->d_state) hipFree(ctx->d_state);
+    if (ctx->d_spill) hipFree(ctx->d_spill);
+    if (ctx->d_params) hipFree(ctx->d_params);
+    if (ctx->d_invalid) hipFree(ctx->d_invalid);
+    delete ctx;
+    return FUTBOL_OK;
+}
+
+extern "C" const char* futbol_last_error(const FutbolCtx* ctx)
+{
+    return ctx ? ctx->err.c_str() : g_create_error.c_str();
+}
+
+extern "C" int futbol_dims(const FutbolCtx* ctx, int32_t* obs_dim, int32_t* action_dim, int32_t* num_envs)
+{
+    if (!ctx) return FUTBOL_EINVAL;
+    if (obs_dim) *obs_dim = ctx->obs_dim;
+    if (action_dim) *action_dim = ctx->act_dim;
+    if (num_envs) *num_envs = ctx->B;
+    return FUTBOL_OK;
+}
+
+extern "C" int futbol_episode_limit(const FutbolCtx* ctx, int32_t* steps)
+{
+    if (!ctx || !steps) return FUTBOL_EINVAL;
+    *steps = ctx->K_done;
+    return FUTBOL_OK;
+}
+
+static int launch(FutbolCtx* ctx, int what, const uint8_t* actions, const uint8_t* mask, void* obs, void* reward,
+                  uint8_t* done, void* term, void* stream)
+{
+    FB_CHECK_HIP(ctx, hipSetDevice(ctx->device));
+    const int out64 = ctx->cfg.out_dtype == FUTBOL_F64;
+    int rc;
+    if (ctx->cfg.env_kind == FUTBOL_ENV_V1)
+        rc = launch_v1(ctx->N, (const V1Params*)ctx->d_params, ctx->B, ctx->v1, out64, what, actions, mask, obs,
+                       reward, done, term, 0, (hipStream_t)stream);
+    else
+        rc = launch_v0((const V0Params*)ctx->d_params, ctx->B, ctx->v0, out64, what, actions, mask, obs, reward,
+                       done, term, 0, (hipStream_t)stream);
+    if (rc) {
+        hipError_t e = hipGetLastError();
+        return fail(ctx, FUTBOL_EHIP, std::string("kernel launch failed: ") + hipGetErrorString(e));
+    }
+    return FUTBOL_OK;
+}
+
+extern "C" int futbol_reset(FutbolCtx* ctx, const uint8_t* mask, void* obs, void* stream)
+{
+    if (!ctx) return FUTBOL_EINVAL;
+    return launch(ctx, 1, nullptr, mask, obs, nullptr, nullptr, nullptr, stream);
+}
+
+extern "C" int futbol_step(FutbolCtx* ctx, const uint8_t* actions, void* obs, void* reward, uint8_t* done,
+                           void* terminal_obs, void* stream)
+{
+    if (!ctx) return FUTBOL_EINVAL;
+    if (!actions || !obs || !reward || !done) return fail(ctx, FUTBOL_EINVAL, "null buffer");
+    int rc = launch(ctx, 0, actions, nullptr, obs, reward, done, terminal_obs, stream);
+    if (rc == FUTBOL_OK) ctx->steps_since_clear += (double)ctx->B;
+    return rc;
+}
+
+extern "C" int futbol_fill_actions(FutbolCtx* ctx, uint64_t seed, uint64_t step, uint8_t* actions, void* stream)
+{
+    if (!ctx || !actions) return FUTBOL_EINVAL;
+    FB_CHECK_HIP(ctx, hipSetDevice(ctx->device));
+    int nvals = 5;  // MultiDiscrete([5, 5] * N) (envs_v1/futbol_env.py:78-79)
+    if (ctx->cfg.env_kind == FUTBOL_ENV_V0) nvals = ctx->cfg.action_as_int0 ? 16 : 4;  // Discrete(16) / Tuple(4, 4)
+    const unsigned long long* ctr = step == ~(uint64_t)0 ? ctx->d_invalid + 1 : nullptr;
+    if (launch_fill_actions(seed, step, ctr, (uint32_t)ctx->env_base, ctx->B, ctx->act_dim, nvals, actions,
+                            (hipStream_t)stream))
+        return fail(ctx, FUTBOL_EHIP, "fill_actions launch failed");
+    return FUTBOL_OK;
+}
+
+extern "C" int futbol_episode_stats(FutbolCtx* ctx, double* out3, int32_t clear, void* stream)
+{
+    if (!ctx || !out3) return FUTBOL_EINVAL;
+    FB_CHECK_HIP(ctx, hipSetDevice(ctx->device));
+    double* sr = ctx->cfg.env_kind == FUTBOL_ENV_V1 ? ctx->v1.stat_ret : ctx->v0.stat_ret;
+    uint32_t* sc = ctx->cfg.env_kind == FUTBOL_ENV_V1 ? ctx->v1.stat_cnt : ctx->v0.stat_cnt;
+    if (launch_episode_stats(sr, sc, ctx->B, ctx->steps_since_clear, out3, clear, sr, sc, (hipStream_t)stream))
+        return fail(ctx, FUTBOL_EHIP, "episode_stats launch failed");
+    if (clear) ctx->steps_since_clear = 0.0;
+    return FUTBOL_OK;
+}
+
+extern "C" int futbol_invalid_actions(FutbolCtx* ctx, uint64_t* out, void* stream)
+{
+    if (!ctx || !out) return FUTBOL_EINVAL;
+    FB_CHECK_HIP(ctx, hipSetDevice(ctx->device));
+    unsigned long long v = 0;
+    FB_CHECK_HIP(ctx, hipMemcpyAsync(&v, ctx->d_invalid, sizeof(v), hipMemcpyDeviceToHost, (hipStream_t)stream));
+    FB_CHECK_HIP(ctx, hipStreamSynchronize((hipStream_t)stream));
+    *out = v;
+    return FUTBOL_OK;
+}
+
+extern "C" int futbol_state_bytes(const FutbolCtx* ctx, size_t* bytes)
+{
+    if (!ctx || !bytes) return FUTBOL_EINVAL;
+    *bytes = ctx->state_bytes;
+    return FUTBOL_OK;
+}
+
+extern "C" int futbol_state_field(const FutbolCtx* ctx, int32_t index, const char** name, size_t* offset,
+                                  int32_t* type_code, int64_t* count)
+{
+    if (!ctx || index < 0 || index >= (int32_t)ctx->fields.size()) return FUTBOL_EINVAL;
+    const Field& f = ctx->fields[index];
+    if (name) *name = f.name;
+    if (offset) *offset = f.offset;
+    if (type_code) *type_code = f.type;
+    if (count) *count = f.count;
+    return FUTBOL_OK;
+}
+
+extern "C" int futbol_get_state(FutbolCtx* ctx, void* dst, int32_t dst_is_host, void* stream)
+{
+    if (!ctx || !dst) return FUTBOL_EINVAL;
+    FB_CHECK_HIP(ctx, hipSetDevice(ctx->device));
+    FB_CHECK_HIP(ctx, hipMemcpyAsync(dst, ctx->d_state, ctx->state_bytes,
+                                     dst_is_host ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice,
+                                     (hipStream_t)stream));
+    if (dst_is_host) FB_CHECK_HIP(ctx, hipStreamSynchronize((hipStream_t)stream));
+    return FUTBOL_OK;
+}
+
+extern "C" int futbol_set_state(FutbolCtx* ctx, const void* src, int32_t src_is_host, void* stream)
+{
+    if (!ctx || !src) return FUTBOL_EINVAL;
+    FB_CHECK_HIP(ctx, hipSetDevice(ctx->device));
+    FB_CHECK_HIP(ctx, hipMemcpyAsync(ctx->d_state, src, ctx->state_bytes,
+                                     src_is_host ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice,
+                                     (hipStream_t)stream));
+    if (src_is_host) FB_CHECK_HIP(ctx, hipStreamSynchronize((hipStream_t)stream));
+    return FUTBOL_OK;
+}

@@ -1,0 +1,56 @@
+// futbol_kernels.hpp -- launch interface between the C ABI (futbol_capi.hip)
+// and the env kernels (futbol_v1.hip, futbol_v0.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+#include "futbol_state.hpp"
+
+namespace futbol {
+
+// Per-context constants of an envs_v1 `Futbol` (kernel argument, < 2 KB).
+struct V1Params {
+    double W, H;                                  // Futbol(width, height)
+    double sax[12], say[12], sbx[12], sby[12];    // _setup_walls segments 0..11 (futbol_env.py:182-234)
+    double sl[12], sb[12], sr[12], st[12];        // their cpBBs (radius 1 included)
+    double fx[21], fy[21];                        // formation of bodies A.., B.., ball (team.py:52-112)
+    double dtv[3];                                // dt per dt code: {0, 1e-4, 0.1}
+    double damp[3];                               // cpfpow(damping 0.95, dt)
+    double biasc[3];                              // 1 - cpfpow(collisionBias, dt)
+    double slop;                                  // collisionSlop (0.1f)
+    uint64_t seed;
+    uint32_t env_base;                            // global id of env 0
+    int B;
+    int K_done;                                   // steps until current_time > total_time
+    int auto_reset;
+};
+
+struct V0Params {
+    double length, width, goal_size, player_speed, shoot_speed;
+    int ty_lo, ty_hi;                             // randint bounds of target_y (:306)
+    int shoot_lo, shoot_hi;                       // randint bounds of the shot speed (:367)
+    int one_goal_end, only_reward_goal, random_opp, action_as_int;
+    uint64_t seed;
+    uint32_t env_base;
+    int B;
+    int K_done;                                   // steps until time >= game_time
+    int auto_reset;
+};
+
+// P: device pointer to the context's V1Params (wave-uniform scalar loads)
+int launch_v1(int N, const V1Params* P, int B, const V1Ptrs& st, int out64, int what, const uint8_t* actions,
+              const uint8_t* mask, void* obs, void* reward, uint8_t* done, void* term, int init,
+              hipStream_t stream);
+int v1_supported(int N);
+size_t v1_spill_slots(int N);
+
+int launch_v0(const V0Params* P, int B, const V0Ptrs& st, int out64, int what, const uint8_t* actions,
+              const uint8_t* mask, void* obs, void* reward, uint8_t* done, void* term, int init,
+              hipStream_t stream);
+
+int launch_fill_actions(uint64_t seed, uint64_t step, const unsigned long long* step_ctr, uint32_t env_base, int B,
+                        int adim, int nvals, uint8_t* actions, hipStream_t stream);
+int launch_episode_stats(const double* stat_ret, const uint32_t* stat_cnt, int B, double steps, double* out3,
+                         int clear, double* stat_ret_w, uint32_t* stat_cnt_w, hipStream_t stream);
+
+}  // namespace futbol

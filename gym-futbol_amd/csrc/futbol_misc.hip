@@ -1,0 +1,77 @@
+// futbol_misc.hip -- synthetic action generation and episode-statistics reduction.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "futbol_kernels.hpp"
+#include "futbol_rng.hpp"
+
+namespace futbol {
+
+// actions[i][j] = floor(U * nvals), U = draw j of (seed, env_base + i, event = step, tag 1):
+// the benchmark's "left agent" (random_action() for the left team, envs_v1/futbol_env.py:306-307)
+// step_ctr != nullptr: use the device counter (advanced by every step launch) instead of `step`,
+// so a captured hipGraph draws fresh actions at every replay.
+__global__ void __launch_bounds__(256) fill_actions_kernel(uint64_t seed, uint32_t step, const unsigned long long* step_ctr,
+                                                           uint32_t env_base, int B, int adim, int nvals,
+                                                           uint8_t* __restrict__ actions)
+{
+    const int env = blockIdx.x * blockDim.x + threadIdx.x;
+    if (env >= B) return;
+    const uint32_t s = step_ctr ? (uint32_t)*step_ctr : step;
+    Stream rs(seed, env_base + (uint32_t)env, s, 1);
+    for (int j = 0; j < adim; ++j) actions[(size_t)env * adim + j] = (uint8_t)rs.choice(nvals);
+}
+
+int launch_fill_actions(uint64_t seed, uint64_t step, const unsigned long long* step_ctr, uint32_t env_base, int B,
+                        int adim, int nvals, uint8_t* actions, hipStream_t stream)
+{
+    hipLaunchKernelGGL(fill_actions_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, seed, (uint32_t)step,
+                       step_ctr, env_base, B, adim, nvals, actions);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// One block, fixed reduction order: reproducible sums.
+__global__ void __launch_bounds__(1024) episode_stats_kernel(const double* __restrict__ ret,
+                                                             const uint32_t* __restrict__ cnt, int B, double steps,
+                                                             double* __restrict__ out3, int clear,
+                                                             double* ret_w, uint32_t* cnt_w)
+{
+    __shared__ double sr[1024];
+    __shared__ double sc[1024];
+    double a = 0.0, c = 0.0;
+    for (int i = threadIdx.x; i < B; i += blockDim.x) {
+        a += ret[i];
+        c += (double)cnt[i];
+    }
+    sr[threadIdx.x] = a;
+    sc[threadIdx.x] = c;
+    __syncthreads();
+    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) {
+            sr[threadIdx.x] += sr[threadIdx.x + s];
+            sc[threadIdx.x] += sc[threadIdx.x + s];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        out3[0] = sr[0];
+        out3[1] = sc[0];
+        out3[2] = steps;
+    }
+    if (clear) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < B; i += blockDim.x) {
+            ret_w[i] = 0.0;
+            cnt_w[i] = 0;
+        }
+    }
+}
+
+int launch_episode_stats(const double* stat_ret, const uint32_t* stat_cnt, int B, double steps, double* out3,
+                         int clear, double* stat_ret_w, uint32_t* stat_cnt_w, hipStream_t stream)
+{
+    hipLaunchKernelGGL(episode_stats_kernel, dim3(1), dim3(1024), 0, stream, stat_ret, stat_cnt, B, steps, out3,
+                       clear, stat_ret_w, stat_cnt_w);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace futbol

@@ -1,0 +1,548 @@
+// futbol_v0.hip -- v0 `FutbolEnv` step (gym_futbol/envs/futbol_env.py) as one
+// HIP kernel for gfx950, including the hard-coded opponent team
+// (`_opp_team_set_vector_observation`, :864-983) and `Easy_Agent.get_action_type`
+// (envs/easy_agent.py:53-98).  One env per lane, the 5 obs rows (25 fp64) in
+// registers; agent indices are template constants so no per-lane array is ever
+// indexed dynamically.  Randomness: the Philox tape of futbol_rng.hpp, drawn in
+// the reference's program order.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "futbol_kernels.hpp"
+#include "futbol_rng.hpp"
+#include "futbol_state.hpp"
+#include "futbol_util.hpp"
+
+namespace futbol {
+namespace v0 {
+
+// module constants, envs/futbol_env.py:18-58
+constexpr double FIELD_LEN = 105.0, FIELD_WID = 68.0;
+constexpr double GOAL_UPPER = FIELD_WID / 2 + 10.0 / 2, GOAL_LOWER = FIELD_WID / 2 - 10.0 / 2;
+constexpr double STEP_SIZE = 0.1;
+constexpr int SHOOT_SPEED = 20;
+enum { AI_1 = 0, AI_2 = 1, OPP_1 = 2, OPP_2 = 3, NOONE = 4 };  // ballowner.py
+enum { RUN = 0, INTERCEPT = 1, SHOOT = 2, ASSIST = 3 };          // action.py
+constexpr int BALL = 4;
+constexpr int MATE[4] = {1, 0, 3, 2};
+constexpr int kViewsLive = 6, kRowValid = 7;
+
+struct Env {
+    double r[5][5];
+    uint32_t owner, last_owner;
+    bool views_live;
+    bool pending_done;
+};
+
+// get_vec (:62-65): vector from o to t and its magnitude
+__device__ __forceinline__ double get_vec(double tx, double ty, double ox, double oy, double& vx, double& vy)
+{
+    vx = tx - ox;
+    vy = ty - oy;
+    return sqrt(vx * vx + vy * vy);
+}
+
+__device__ __forceinline__ double intercept_chance(double d) /* :122-129, d1 = 1, d2 = 2 */
+{
+    if (d < 1.0) return 0.9;
+    if (d >= 1.0 && d <= 2.0) {
+        const double k = 0.9 / (1.0 - 2.0);
+        return k * (d - 2.0);
+    }
+    return 0.0;
+}
+
+struct Ctx {
+    const V0Params* P;
+    double* view;
+    int env, B;
+    Stream* rs;
+};
+
+__device__ __forceinline__ void load_view(const Ctx& c, int a, double& x, double& y)
+{
+    x = c.view[(size_t)(2 * a) * c.B + c.env];
+    y = c.view[(size_t)(2 * a + 1) * c.B + c.env];
+}
+
+// defence_near (:280-289) with the agent's (possibly stale) Easy_Agent view
+template <int a>
+__device__ __forceinline__ int defence_near(const Ctx& c, const Env& e)
+{
+    double vx, vy;
+    const bool live = a < 2 ? e.views_live : (!c.P->random_opp || e.views_live);
+    if (live) {
+        vx = e.r[a][0];
+        vy = e.r[a][1];
+    } else {
+        load_view(c, a, vx, vy);
+    }
+    constexpr int o = a < 2 ? 2 : 0;
+    double t0, t1;
+    const double d1 = get_vec(e.r[o][0], e.r[o][1], vx, vy, t0, t1);
+    const double d2 = get_vec(e.r[o + 1][0], e.r[o + 1][1], vx, vy, t0, t1);
+    if (d1 <= 2 && d2 <= 2) return 2;  // bigger_than (:76-82)
+    if (d1 > 2 && d2 > 2) return 0;
+    return 1;
+}
+
+// _set_vector_observation (:300-530)
+template <int a>
+__device__ __forceinline__ void set_vector_observation(const Ctx& c, Env& e, bool has_ball, int action,
+                                                       bool set_target, double tgx, double tgy)
+{
+    constexpr bool right = a >= 2;
+    const V0Params* P = c.P;
+    double* ag = e.r[a];
+    double* ball = e.r[BALL];
+    const double target_y = (double)c.rs->randint(P->ty_lo, P->ty_hi);
+    if (has_ball) {
+        if (action == INTERCEPT) {
+            ag[2] = 0; ag[3] = 0; ag[4] = 0;
+            ball[2] = 0; ball[3] = 0; ball[4] = 0;
+        } else if (action == RUN) {
+            ag[4] = P->player_speed;
+            if (set_target) {
+                ag[2] = tgx;
+                ag[3] = tgy;
+            } else {
+                double vx, vy;
+                get_vec(right ? 0.0 : P->length, target_y, ag[0], ag[1], vx, vy);
+                ag[2] = vx;
+                ag[3] = vy;
+            }
+            if (c.rs->uniform01() < 0.05) e.owner = NOONE;
+            else {
+#pragma unroll
+                for (int f = 0; f < 5; ++f) ball[f] = ag[f];
+            }
+        } else if (action == SHOOT) {
+            const int acc = 10 + defence_near<a>(c, e) * 20;
+            ball[4] = c.rs->randint(P->shoot_lo, P->shoot_hi) * 1.0;
+            double vx, vy;
+            const double mag = get_vec(right ? 0.0 : P->length, target_y, ball[0], ball[1], vx, vy);
+            // screw_vec (:101-116): one normal draw, then randint(0, 9) for the index
+            const double nd = c.rs->normal(0.0, (double)acc);
+            const double cs = vx * 1.0 / mag, sn = vy * 1.0 / mag;
+            (void)c.rs->randint(0, 9);
+            const double ang = (nd / 180) * 3.141592653589793;
+            double ss, sc;
+            pm_sincos(ang, &ss, &sc);
+            const double tc = (cs * sc) - (sn * ss), ts = (sn * sc) + (cs * ss);
+            ball[2] = tc * mag;
+            ball[3] = ts * mag;
+            e.last_owner = e.owner;
+            e.owner = NOONE;
+            ag[2] = 0; ag[3] = 0; ag[4] = 0;
+        } else {  // ASSIST
+            const double* mate = e.r[MATE[a]];
+            double vx, vy;
+            const double mag = get_vec(mate[0], mate[1], ball[0], ball[1], vx, vy);
+            double cps = mag / STEP_SIZE;
+            if (cps > SHOOT_SPEED) cps = SHOOT_SPEED;
+            ball[4] = c.rs->uniform(cps - 1, cps + 1);
+            ball[2] = vx;
+            ball[3] = vy;
+            e.last_owner = e.owner;
+            e.owner = NOONE;
+            ag[2] = 0; ag[3] = 0; ag[4] = 0;
+        }
+    } else {
+        double btax, btay, gtax, gtay;
+        const double btam = get_vec(ball[0], ball[1], ag[0], ag[1], btax, btay);
+        get_vec(right ? 0.0 : P->length, P->width / 2, ag[0], ag[1], gtax, gtay);
+        if (action == INTERCEPT) {
+            const bool success = c.rs->uniform01() < intercept_chance(btam);
+            if (success || (e.owner == NOONE && btam < 2 + 2)) {
+                ball[2] = ag[2]; ball[3] = ag[3]; ball[4] = ag[4];
+                ball[0] = ag[0]; ball[1] = ag[1];
+                e.last_owner = e.owner;
+                e.owner = a;
+            }
+        } else if (action == RUN) {
+            ag[4] = P->player_speed;
+            if (set_target) { ag[2] = tgx; ag[3] = tgy; }
+            else if (e.owner != (uint32_t)a) { ag[2] = btax; ag[3] = btay; }
+            else { ag[2] = gtax; ag[3] = gtay; }
+        } else {
+            ag[2] = 0; ag[3] = 0; ag[4] = 0;
+        }
+    }
+}
+
+// Easy_Agent.get_action_type (easy_agent.py:53-98), shoot_range = 20 (futbol_env.py:196-201)
+template <int a>
+__device__ __forceinline__ int get_action_type(const Ctx& c, const Env& e, bool has_ball, bool team_has_ball)
+{
+    constexpr bool right = a >= 2;
+    const double* ag = e.r[a];
+    const double* mate = e.r[MATE[a]];
+    const double* ball = e.r[BALL];
+    double t0, t1;
+    const double btam = get_vec(ball[0], ball[1], ag[0], ag[1], t0, t1);
+    const double mtam = get_vec(mate[0], mate[1], ag[0], ag[1], t0, t1);
+    const double shoot_x = right ? 0.0 + 20 : c.P->length - 20;
+    if (has_ball) {
+        if ((right && ag[0] <= shoot_x) || (!right && ag[0] >= shoot_x)) return SHOOT;
+        if ((mate[0] < ag[0] || mate[1] < ag[1] - 7 || mate[1] > ag[1] + 7) && c.rs->uniform01() > 0.8 && mtam > 12)
+            return ASSIST;
+        return RUN;
+    }
+    if (btam <= 1 && !team_has_ball) return INTERCEPT;
+    return RUN;
+}
+
+// _step_by_observation (:560-571); DECELERATION = 0
+__device__ __forceinline__ void step_by_observation(double* o)
+{
+    const double tx = o[2], ty = o[3];
+    const double mag = sqrt(tx * tx + ty * ty);
+    if (mag != 0) {
+        o[0] = o[0] + o[4] * (tx * STEP_SIZE / mag);
+        o[1] = o[1] + o[4] * (ty * STEP_SIZE / mag);
+    }
+}
+
+// _opp_team_set_vector_observation (:864-983)
+__device__ __forceinline__ void opp_team(const Ctx& c, Env& e)
+{
+    const V0Params* P = c.P;
+    const bool o1has = e.owner == OPP_1, o2has = e.owner == OPP_2;
+    const bool team = o1has || o2has;
+    int a1 = get_action_type<OPP_1>(c, e, o1has, team);
+    int a2 = get_action_type<OPP_2>(c, e, o2has, team);
+    const int opp1_action = a1, opp2_action = a2;  // the Action enums keep the pre-override values (D.13)
+    bool s1 = false, s2 = false;
+    double t1x = 0, t1y = 0, t2x = 0, t2y = 0;
+    double* o1 = e.r[OPP_1];
+    double* o2 = e.r[OPP_2];
+    if (o1has && opp1_action == RUN) {
+        if (o1[1] > P->width * 0.2) { s1 = true; t1x = -1; t1y = -1; }
+        if (opp2_action == RUN && o2[0] > P->length * 0.1)
+            if (o2[1] < P->width * 0.8) { s2 = true; t2x = -1; t2y = 1; }
+    }
+    if (o2has && opp2_action == RUN) {
+        if (o2[1] < P->width * 0.8) { s2 = true; t2x = -1; t2y = 1; }
+        if (opp1_action == RUN && o1[0] > P->length * 0.1)
+            if (o1[1] > P->width * 0.2) { s1 = true; t1x = -1; t1y = -1; }
+    }
+    if (e.owner == AI_1 || e.owner == AI_2) {
+        if (e.r[BALL][0] < P->length * 0.6) {
+            const double dpx = P->length * 0.75, dpy = P->width * 0.5;
+            if (o1[0] > o2[0]) { a1 = RUN; s1 = true; get_vec(dpx, dpy, o1[0], o1[1], t1x, t1y); }
+            else { a2 = RUN; s2 = true; get_vec(dpx, dpy, o2[0], o2[1], t2x, t2y); }
+        }
+    }
+    set_vector_observation<OPP_1>(c, e, o1has, a1, s1, t1x, t1y);
+    set_vector_observation<OPP_2>(c, e, o2has, a2, s2, t2x, t2y);
+    if (e.owner == NOONE && opp1_action == RUN && opp2_action == RUN) {
+        // anticipate the ball (:962-982)
+        double nb[5];
+#pragma unroll
+        for (int f = 0; f < 5; ++f) nb[f] = e.r[BALL][f];
+        step_by_observation(nb);
+        double v1x, v1y, v2x, v2y;
+        const double m1 = get_vec(nb[0], nb[1], o1[0], o1[1], v1x, v1y);
+        const double m2 = get_vec(nb[0], nb[1], o2[0], o2[1], v2x, v2y);
+        if (m1 < STEP_SIZE * P->player_speed) { o1[2] = v1x; o1[3] = v1y; o1[4] = m1 / STEP_SIZE; }
+        else if (m2 < STEP_SIZE * P->player_speed) { o2[2] = v2x; o2[3] = v2y; o2[4] = m2 / STEP_SIZE; }
+    }
+}
+
+__device__ __forceinline__ bool obj_out(const double* o) /* out, :574-577 */
+{
+    return (o[0] < 0 || o[0] > FIELD_LEN) || (o[1] < 0 || o[1] > FIELD_WID);
+}
+
+__device__ __forceinline__ bool score(const Env& e) /* :580-583 */
+{
+    const double* b = e.r[BALL];
+    const bool ai_in = b[0] <= 0 && (b[1] > GOAL_LOWER && b[1] < GOAL_UPPER);
+    const bool opp_in = b[0] >= FIELD_LEN && (b[1] > GOAL_LOWER && b[1] < GOAL_UPPER);
+    return ai_in || opp_in;
+}
+
+// _get_reward (:752-861); ob/oa1/oa2/oown: copies taken at the top of step()
+__device__ __forceinline__ double get_reward(const V0Params* P, const Env& e, const double* ob, const double* oa1,
+                                             const double* oa2, const double* oown, int act1, int act2)
+{
+    double t0, t1;
+    const double b2a1 = get_vec(ob[0], ob[1], oa1[0], oa1[1], t0, t1);
+    const double b2a2 = get_vec(ob[0], ob[1], oa2[0], oa2[1], t0, t1);
+    const double running_r = (act1 == RUN || act2 == RUN) ? 10 * 0.2 : 0;
+    const double player_adv_r = ((oown[0] == 10 && act2 == RUN) || (oown[1] == 10 && act1 == RUN)) ? 10 * 0.2 : 0;
+    double bad1, bad2;
+    if (oown[0] == 0) {
+        if (act1 == ASSIST || act1 == SHOOT) bad1 = 2 * -0.5;
+        else if (b2a1 > 2 && act1 == INTERCEPT) bad1 = 1 * -0.5;
+        else bad1 = 0;
+    } else bad1 = act1 == INTERCEPT ? 2 * -0.5 : 0;
+    if (oown[1] == 0) {
+        if (act2 == ASSIST || act2 == SHOOT) bad2 = 2 * -0.5;
+        else if (b2a2 > 2 && act1 == INTERCEPT) bad2 = 1 * -0.5;  // the reference tests action1 (D.9)
+        else bad2 = 0;
+    } else bad2 = act2 == INTERCEPT ? 2 * -0.5 : 0;
+    const double bad = bad1 + bad2;
+    const double oof = (obj_out(e.r[AI_1]) || obj_out(e.r[AI_2])) ? -0.6 : 0;
+    double get_ball;
+    if ((e.owner == AI_1 || e.owner == AI_2) && (oown[0] == 0 && oown[1] == 0)) {
+        if (ob[2] > ob[3] && ob[2] > 0 && ob[0] > oa1[0] && ob[0] > oa2[0] && oown[4] == 10) get_ball = -50 * 0.3;
+        else get_ball = 60 * 0.3;
+    } else if ((e.owner == AI_1 && oown[0] == 10) || (e.owner == AI_2 && oown[1] == 10)) {
+        get_ball = 30 * 0.3;
+    } else get_ball = 0;
+    const bool sc = score(e);
+    const double s = (sc && e.r[BALL][0] >= FIELD_LEN) ? 1000 : 0;
+    const double gs = (sc && e.r[BALL][0] <= 0) ? -1000 : 0;
+    if (P->only_reward_goal) return s + gs;
+    return get_ball + s + gs + oof + bad + player_adv_r + running_r;
+}
+
+__device__ __forceinline__ void formation(Env& e)
+{
+    constexpr double init[5][2] = {{FIELD_LEN / 2 - 9, FIELD_WID / 2 + 5}, {FIELD_LEN / 2 - 9, FIELD_WID / 2 - 5},
+                                   {FIELD_LEN / 2 + 9, FIELD_WID / 2 + 5}, {FIELD_LEN / 2 + 9, FIELD_WID / 2 - 5},
+                                   {FIELD_LEN / 2, FIELD_WID / 2}};
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+        e.r[r][0] = init[r][0];
+        e.r[r][1] = init[r][1];
+        e.r[r][2] = 0;
+        e.r[r][3] = 0;
+        e.r[r][4] = 0;
+    }
+    e.owner = NOONE;
+    e.last_owner = NOONE;
+}
+
+// self.obs re-bound (reset() / goal): Easy_Agent views still point at the old array
+__device__ __forceinline__ void rebind(const Ctx& c, Env& e)
+{
+    if (e.views_live) {
+        e.views_live = false;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            c.view[(size_t)(2 * a) * c.B + c.env] = e.r[a][0];
+            c.view[(size_t)(2 * a + 1) * c.B + c.env] = e.r[a][1];
+        }
+    }
+}
+
+template <typename OT>
+__device__ __forceinline__ void write_obs(const Env& e, bool row_valid, OT* o)
+{
+#pragma unroll
+    for (int r = 0; r < 5; ++r)
+#pragma unroll
+        for (int f = 0; f < 5; ++f) o[r * 5 + f] = (OT)e.r[r][f];
+    const int idx = e.owner <= 3 ? (int)e.owner : 4;  // ball_owner_array_update (:720-736)
+#pragma unroll
+    for (int f = 0; f < 5; ++f) o[25 + f] = (OT)((row_valid && f == idx) ? 10 : 0);
+}
+
+__device__ __forceinline__ void load(const V0Ptrs& st, int env, int B, Env& e, Meta& m)
+{
+#pragma unroll
+    for (int r = 0; r < 5; ++r)
+#pragma unroll
+        for (int f = 0; f < 5; ++f) e.r[r][f] = st.row[(size_t)(r * 5 + f) * B + env];
+    m.w = st.meta[env];
+    e.owner = m.owner();
+    e.last_owner = m.last_owner();
+    e.views_live = m.bit(kViewsLive);
+    e.pending_done = false;
+}
+
+__device__ __forceinline__ void store(const V0Ptrs& st, int env, int B, const Env& e, Meta& m, bool row_valid)
+{
+#pragma unroll
+    for (int r = 0; r < 5; ++r)
+#pragma unroll
+        for (int f = 0; f < 5; ++f) st.row[(size_t)(r * 5 + f) * B + env] = e.r[r][f];
+    m.set_owner(e.owner);
+    m.set_last_owner(e.last_owner);
+    m.set_bit(kViewsLive, e.views_live);
+    m.set_bit(kRowValid, row_valid);
+    st.meta[env] = m.w;
+}
+
+}  // namespace v0
+
+using namespace v0;
+
+// FutbolEnv.step (:628-717) + DummyVecEnv auto-reset
+template <typename OT>
+__global__ void __launch_bounds__(64) v0_step_kernel(const V0Params* __restrict__ P, V0Ptrs st,
+                                                     const uint8_t* __restrict__ actions, OT* __restrict__ obs,
+                                                     OT* __restrict__ reward, uint8_t* __restrict__ done_out,
+                                                     OT* __restrict__ term_obs)
+{
+    const int env = blockIdx.x * 64 + threadIdx.x;
+    const int B = P->B;
+    if (env >= B) return;
+    Env e;
+    Meta m;
+    load(st, env, B, e, m);
+    const bool row_valid_before = m.bit(kRowValid);
+    const uint32_t ev = m.event();
+    m.set_event(ev + 1);
+    Stream rs(P->seed, P->env_base + (uint32_t)env, ev, 0);
+    const Ctx c{P, st.view, env, B, &rs};
+
+    int a0, a1, bad = 0;
+    if (P->action_as_int) {
+        int a = actions[env];
+        bad = a > 15;
+        a = a > 15 ? 15 : a;
+        a0 = a / 4;
+        a1 = a % 4;
+    } else {
+        a0 = actions[(size_t)env * 2];
+        a1 = actions[(size_t)env * 2 + 1];
+        bad = (a0 > 3) + (a1 > 3);
+        a0 = a0 > 3 ? 3 : a0;
+        a1 = a1 > 3 ? 3 : a1;
+    }
+    if (bad) atomicAdd(st.invalid, (unsigned long long)bad);
+
+    double ob[5], oa1[5], oa2[5], oown[5];
+    const int oidx = e.owner <= 3 ? (int)e.owner : 4;
+#pragma unroll
+    for (int f = 0; f < 5; ++f) {
+        ob[f] = e.r[BALL][f];
+        oa1[f] = e.r[AI_1][f];
+        oa2[f] = e.r[AI_2][f];
+        oown[f] = (row_valid_before && f == oidx) ? 10 : 0;
+    }
+
+    if (P->random_opp) {
+        const int t = rs.randint(0, 15);
+        set_vector_observation<OPP_1>(c, e, e.owner == OPP_1, t / 4, false, 0, 0);
+        set_vector_observation<OPP_2>(c, e, e.owner == OPP_2, t % 4, false, 0, 0);
+    } else {
+        opp_team(c, e);
+    }
+    set_vector_observation<AI_1>(c, e, e.owner == AI_1, a0, false, 0, 0);
+    set_vector_observation<AI_2>(c, e, e.owner == AI_2, a1, false, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 5; ++r) step_by_observation(e.r[r]);
+
+    const double rw = get_reward(P, e, ob, oa1, oa2, oown, a0, a1);
+    bool done = false;
+    if (score(e)) {
+        const int who = e.r[BALL][0] <= 0 ? 1 : 0;
+        st.score[(size_t)who * B + env] = st.score[(size_t)who * B + env] + 1;
+        if (P->one_goal_end) done = true;
+        rebind(c, e);
+        formation(e);
+    }
+    {  // out_of_field (:621-625) + fix (:587-604)
+        double* b = e.r[BALL];
+        const bool x_out = b[0] < 0 || b[0] > P->length;
+        const bool y_out = b[1] < 0 || b[1] > P->width;
+        const double gd = P->width / 2 - P->goal_size / 2, gu = P->width / 2 + P->goal_size / 2;
+        const bool y_score = b[1] > gd - 2 && b[1] < gu + 2;
+        if ((x_out && !y_score) || y_out) {
+            const uint32_t nw = (e.last_owner == OPP_1 || e.last_owner == OPP_2) ? AI_1 : OPP_1;
+            b[0] = b[0] < 0 ? 0.0 : (b[0] > FIELD_LEN ? FIELD_LEN : b[0]);
+            b[1] = b[1] < 0 ? 0.0 : (b[1] > FIELD_WID ? FIELD_WID : b[1]);
+            e.owner = nw;
+            b[2] = 0; b[3] = 0; b[4] = 0;
+            if (nw == AI_1) {
+#pragma unroll
+                for (int f = 0; f < 5; ++f) e.r[AI_1][f] = b[f];
+            } else {
+#pragma unroll
+                for (int f = 0; f < 5; ++f) e.r[OPP_1][f] = b[f];
+            }
+            if (P->one_goal_end) done = true;
+        }
+    }
+    const uint32_t steps = m.steps();
+    if ((int)steps + 1 >= P->K_done) done = true;  // time >= game_time, checked before time += 0.1
+    m.set_steps(steps + 1 > (uint32_t)kMaxSteps ? (uint32_t)kMaxSteps : steps + 1);
+
+    double ret = st.ep_ret[env] + rw;
+    bool row_valid = true;
+    if (done && !P->auto_reset) {
+        st.stat_ret[env] = st.stat_ret[env] + ret;
+        st.stat_cnt[env] = st.stat_cnt[env] + 1;
+        ret = 0.0;
+    }
+    if (done && P->auto_reset) {
+        if (term_obs) write_obs<OT>(e, true, term_obs + (size_t)env * 30);
+        st.stat_ret[env] = st.stat_ret[env] + ret;
+        st.stat_cnt[env] = st.stat_cnt[env] + 1;
+        ret = 0.0;
+        // reset() (:205-245): new event (no draws), rebind, formation, time/scores 0
+        m.set_event(m.event() + 1);
+        rebind(c, e);
+        formation(e);
+        m.set_steps(0);
+        st.score[env] = 0;
+        st.score[(size_t)B + env] = 0;
+        row_valid = false;
+    }
+    write_obs<OT>(e, row_valid, obs + (size_t)env * 30);
+    st.ep_ret[env] = ret;
+    reward[env] = (OT)rw;
+    done_out[env] = done ? 1 : 0;
+    store(st, env, B, e, m, row_valid);
+    if (env == 0) *st.act_step += 1;
+}
+
+template <typename OT>
+__global__ void __launch_bounds__(64) v0_reset_kernel(const V0Params* __restrict__ P, V0Ptrs st,
+                                                      const uint8_t* __restrict__ mask, OT* __restrict__ obs,
+                                                      int init)
+{
+    const int env = blockIdx.x * 64 + threadIdx.x;
+    const int B = P->B;
+    if (env >= B) return;
+    if (mask && !mask[env]) return;
+    Env e;
+    Meta m;
+    Stream rs(P->seed, P->env_base + (uint32_t)env, 0, 0);
+    const Ctx c{P, st.view, env, B, &rs};
+    if (init) {
+        // __init__: self.obs = self.reset() (event 0, no draws); agents hold live views into it
+        formation(e);
+        m.w = 0;
+        m.set_event(1);
+        e.views_live = true;
+        st.stat_ret[env] = 0.0;
+        st.stat_cnt[env] = 0;
+    } else {
+        load(st, env, B, e, m);
+        m.set_event(m.event() + 1);
+        rebind(c, e);
+        formation(e);
+    }
+    m.set_steps(0);
+    st.score[env] = 0;
+    st.score[(size_t)B + env] = 0;
+    st.ep_ret[env] = 0.0;
+    if (obs) write_obs<OT>(e, false, obs + (size_t)env * 30);
+    store(st, env, B, e, m, false);
+}
+
+int launch_v0(const V0Params* P, int B, const V0Ptrs& st, int out64, int what, const uint8_t* actions,
+              const uint8_t* mask, void* obs, void* reward, uint8_t* done, void* term, int init, hipStream_t stream)
+{
+    const dim3 grid((B + 63) / 64), block(64);
+    if (what == 0) {
+        if (out64)
+            hipLaunchKernelGGL((v0_step_kernel<double>), grid, block, 0, stream, P, st, actions, (double*)obs,
+                               (double*)reward, done, (double*)term);
+        else
+            hipLaunchKernelGGL((v0_step_kernel<float>), grid, block, 0, stream, P, st, actions, (float*)obs,
+                               (float*)reward, done, (float*)term);
+    } else {
+        if (out64)
+            hipLaunchKernelGGL((v0_reset_kernel<double>), grid, block, 0, stream, P, st, mask, (double*)obs, init);
+        else
+            hipLaunchKernelGGL((v0_reset_kernel<float>), grid, block, 0, stream, P, st, mask, (float*)obs, init);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace futbol

@@ -1,0 +1,16 @@
+"""gym_futbol_amd -- MI355X-native vectorised gym-futbol envs.
+
+The reference's gym ids and APIs (gym_futbol/__init__.py, envs_v1/futbol_env.py,
+envs/futbol_env.py) backed by hand-written HIP kernels for gfx950
+(libfutbol_amd.so, C ABI in include/futbol.h).  See DESIGN.md.
+"""
+from ._native import LIB_PATH, NativeError, load as load_native
+from .registration import ENV_SPECS, make, register_with_gym, spec
+from .vec_env import FutbolVecEnv, SB3VecEnv
+from .envs_v1 import Futbol
+from .envs import FutbolEnv
+
+__all__ = ["make", "spec", "ENV_SPECS", "FutbolVecEnv", "SB3VecEnv", "Futbol", "FutbolEnv", "NativeError",
+           "LIB_PATH", "load_native"]
+
+register_with_gym()

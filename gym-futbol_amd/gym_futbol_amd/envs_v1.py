@@ -1,0 +1,101 @@
+"""`Futbol` -- single-env facade with the reference's envs_v1 API.
+
+Mirrors gym_futbol/envs_v1/futbol_env.py:62-515 (`Futbol`): same constructor
+kwargs, `reset()`, `step(left_player_action) -> (obs, reward, done, {})`,
+`random_action()`, `action_space`, `observation_space`, and the attributes the
+reference's notebook reads (`width`, `height`, `number_of_player`,
+`current_time`, `ball_owner_side`).  The step runs on the GPU (a B = 1
+context, fp64 outputs, no auto-reset: like the reference, `done` stays True if
+one keeps stepping).  For throughput use FutbolVecEnv / make(..., num_envs=B).
+"""
+import numpy as np
+import torch
+
+from .vec_env import FutbolVecEnv
+
+WIDTH, HEIGHT, TOTAL_TIME = 105, 68, 30
+
+
+class Futbol:
+    def __init__(self, width=WIDTH, height=HEIGHT, total_time=TOTAL_TIME, debug=False, number_of_player=5,
+                 device="cuda", seed=0, env_id=0):
+        self.width = width
+        self.height = height
+        self.total_time = total_time
+        self.debug = debug
+        self.number_of_player = number_of_player
+        self._venv = FutbolVecEnv("v1", 1, device=device, seed=seed, env_id_base=env_id, dtype=torch.float64,
+                                  auto_reset=False, number_of_player=number_of_player, width=width, height=height,
+                                  total_time=total_time)
+        self.action_space = self._venv.action_space
+        self.observation_space = self._venv.observation_space
+        # the constructor already ran reset() (envs_v1/futbol_env.py:127)
+        self.observation = observation_from_state(self._venv.get_state(), number_of_player)
+
+    def reset(self):
+        obs = self._venv.reset()
+        self.observation = obs[0].cpu().numpy().copy()
+        return self.observation
+
+    def random_action(self):
+        return self.action_space.sample()
+
+    def step(self, left_player_action):
+        a = np.asarray(left_player_action, dtype=np.int64).reshape(1, -1)
+        if a.shape[1] != 2 * self.number_of_player or (a < 0).any() or (a > 4).any():
+            raise ValueError("invalid action %r for MultiDiscrete([5, 5] * %d)" % (left_player_action,
+                                                                                 self.number_of_player))
+        obs, rew, done, _ = self._venv.step(torch.as_tensor(a, dtype=torch.uint8))
+        self.observation = obs[0].cpu().numpy().copy()
+        return self.observation, float(rew[0].item()), bool(done[0].item()), {}
+
+    # -- attributes of the reference env --------------------------------------
+    @property
+    def current_time(self):
+        steps = int((self._venv.get_state()["meta"][0] >> np.uint64(18)) & np.uint64(0x3FFF))
+        t = 0
+        for _ in range(steps):
+            t += 0.1  # futbol_env.py:478 accumulates in fp64
+        return t
+
+    @property
+    def ball_owner_side(self):
+        return "left" if int(self._venv.get_state()["meta"][0] & np.uint64(7)) == 0 else "right"
+
+    def body_states(self):
+        """(positions [Nb,2], velocities [Nb,2]) of A0.., B0.., ball."""
+        s = self._venv.get_state()
+        return np.stack([s["px"], s["py"]], 1), np.stack([s["vx"], s["vy"]], 1)
+
+    def render(self, ax=None):
+        """Matplotlib drawing of the field (replaces pymunk's debug_draw, futbol_env.py:236-243)."""
+        import matplotlib.pyplot as plt
+        from matplotlib.patches import Circle
+        p, _ = self.body_states()
+        pad = 5
+        if ax is None:
+            ax = plt.axes(xlim=(0 - pad, self.width + pad), ylim=(0 - pad, self.height + pad))
+        ax.set_aspect("equal")
+        n = self.number_of_player
+        w, h, g = self.width, self.height, 20
+        for (x0, y0), (x1, y1) in [((0, 0), (0, h / 2 - g / 2)), ((0, h / 2 + g / 2), (0, h)), ((0, h), (w, h)),
+                                   ((w, 0), (w, h / 2 - g / 2)), ((w, h / 2 + g / 2), (w, h)), ((0, 0), (w, 0))]:
+            ax.plot([x0, x1], [y0, y1], "k-")
+        for k in range(2 * n + 1):
+            color = "g" if k == 2 * n else ("r" if k < n else "b")
+            ax.add_patch(Circle(tuple(p[k]), 1.0 if k == 2 * n else 1.5, color=color))
+        return ax
+
+    def close(self):
+        self._venv.close()
+
+
+def observation_from_state(state, n, env=0):
+    """_get_observation (futbol_env.py:154-180) of env `env` from a host state dict."""
+    nb = 2 * n + 1
+    B = state["meta"].shape[0]
+    px, py, vx, vy = (state[k].reshape(nb, B)[:, env] for k in ("px", "py", "vx", "vy"))
+    o = [(px[-1] - 52.5) / 52.5, (py[-1] - 34.0) / 34.0, (vx[-1] - 0.0) / 25.0, (vy[-1] - 0.0) / 25.0]
+    for k in range(2 * n):
+        o += [(px[k] - 52.5) / 55.5, (py[k] - 34.0) / 34.0, (vx[k] - 0.0) / 10.0, (vy[k] - 0.0) / 10.0]
+    return np.array(o, dtype=np.float64)

@@ -1,0 +1,281 @@
+"""FutbolVecEnv: B independent gym-futbol envs resident on one GPU.
+
+Torch-native, zero-copy: `reset()` / `step(actions)` take and return torch
+tensors on the env's device; every call is one kernel launch on the current
+HIP stream (graph-capturable, no host sync).  `as_sb3()` wraps it in the
+stable-baselines VecEnv interface (numpy in/out, infos with
+`terminal_observation`), which is what the reference's notebook drives through
+DummyVecEnv (colab_notebook.ipynb:818-823).
+
+Semantics per env are those of the reference's `step()`:
+  v1 envs_v1/futbol_env.py:427-483 (opponent = random_action(), in-kernel)
+  v0 envs/futbol_env.py:628-717     (hard-coded or random opponent, in-kernel)
+plus DummyVecEnv's auto-reset: on done, `info["terminal_observation"]` holds the
+episode's last obs and the returned obs is the reset obs.
+"""
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _native as nat
+from . import spaces as sp
+
+_DT = {"f8": np.float64, "u8": np.uint64, "u4": np.uint32, "u2": np.uint16, "u1": np.uint8}
+
+
+def _stream_ptr(device):
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class FutbolVecEnv:
+    """Vectorised env.  kind: "v1" (envs_v1.Futbol) or "v0" (envs.FutbolEnv).
+
+    v1 kwargs: number_of_player, width, height, total_time.
+    v0 kwargs: length, width, goal_size, game_time, player_speed, shoot_speed,
+               one_goal_end, action_as_int, only_reward_goal, random_opp.
+    """
+
+    def __init__(self, kind="v1", num_envs=1, device="cuda", seed=0, env_id_base=0, dtype=torch.float32,
+                 auto_reset=True, **kwargs):
+        if not torch.cuda.is_available():
+            raise nat.NativeError("FutbolVecEnv needs a ROCm GPU (torch.cuda.is_available() is False); "
+                                  "there is no CPU fallback")
+        self.kind = kind
+        self.device = torch.device(device)
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        env_kind = nat.ENV_V1 if kind == "v1" else nat.ENV_V0
+        n = int(kwargs.pop("number_of_player", 2)) if kind == "v1" else 2
+        cfg = nat.default_config(env_kind, n)
+        cfg.out_dtype = nat.F64 if dtype == torch.float64 else nat.F32
+        cfg.auto_reset = 1 if auto_reset else 0
+        v1_keys = {"width": "width", "height": "height", "total_time": "total_time"}
+        v0_keys = {"length": "length0", "width": "width0", "goal_size": "goal_size0", "game_time": "game_time0",
+                   "player_speed": "player_speed0", "shoot_speed": "shoot_speed0",
+                   "one_goal_end": "one_goal_end0", "action_as_int": "action_as_int0",
+                   "only_reward_goal": "only_reward_goal0", "random_opp": "random_opp0"}
+        keys = v1_keys if kind == "v1" else v0_keys
+        for k, v in kwargs.items():
+            if k not in keys:
+                raise TypeError("unexpected keyword argument %r for %s" % (k, kind))
+            setattr(cfg, keys[k], type(getattr(cfg, keys[k]))(v) if not isinstance(v, bool) else int(v))
+        self.number_of_player = n
+        self.seed_value = int(seed)
+        self.env_id_base = int(env_id_base)
+        with torch.cuda.device(self.device):
+            self.ctx = nat.Context(cfg, self.device.index, seed, env_id_base, num_envs)
+        self.num_envs = self.ctx.num_envs
+        self.obs_dim = self.ctx.obs_dim
+        self.action_dim = self.ctx.action_dim
+        self.dtype = dtype
+        self.episode_steps = self.ctx.episode_steps
+        B, dev = self.num_envs, self.device
+        self.obs_shape = (self.obs_dim,) if kind == "v1" else (6, 5)
+        self._obs = torch.zeros((B,) + self.obs_shape, dtype=dtype, device=dev)
+        self._term = torch.zeros((B,) + self.obs_shape, dtype=dtype, device=dev)
+        self._rew = torch.zeros(B, dtype=dtype, device=dev)
+        self._done = torch.zeros(B, dtype=torch.uint8, device=dev)
+        self._act = torch.zeros((B, self.action_dim), dtype=torch.uint8, device=dev)
+        self._stats = torch.zeros(3, dtype=torch.float64, device=dev)
+        if kind == "v1":
+            self.action_space = sp.v1_action_space(n)
+            self.observation_space = sp.v1_observation_space(n)
+        else:
+            self.action_space = sp.v0_action_space(bool(cfg.action_as_int0))
+            self.observation_space = sp.v0_observation_space(cfg.length0, cfg.width0, cfg.player_speed0,
+                                                             cfg.shoot_speed0)
+        self._pending = None
+
+    # ---------------------------------------------------------------- core
+    def _actions_u8(self, actions):
+        a = torch.as_tensor(actions, device=self.device)
+        a = a.reshape(self.num_envs, self.action_dim)
+        if a.dtype != torch.uint8:
+            if bool((a < 0).any()):
+                raise ValueError("negative action")
+            a = a.to(torch.uint8)
+        return a.contiguous()
+
+    def reset(self, mask=None):
+        """reset() every env (or those with mask[i] != 0); returns obs [B, ...] (device tensor)."""
+        m = None
+        if mask is not None:
+            m = torch.as_tensor(mask, device=self.device).to(torch.uint8).contiguous()
+        with torch.cuda.device(self.device):
+            nat.check(nat.load().futbol_reset(self.ctx.h, None if m is None else m.data_ptr(),
+                                              self._obs.data_ptr(), _stream_ptr(self.device)), self.ctx.h)
+        return self._obs
+
+    def step(self, actions):
+        """step(actions [B, action_dim]) -> (obs, reward, done(bool), info) as device tensors.
+
+        The returned tensors are the env's own buffers and are overwritten by the
+        next call (clone them to keep them).  info["terminal_observation"] is valid
+        for the rows where done is True."""
+        a = actions if (isinstance(actions, torch.Tensor) and actions.dtype == torch.uint8
+                        and actions.is_contiguous() and actions.device == self.device) else self._actions_u8(actions)
+        self.step_raw(a)
+        return self._obs, self._rew, self._done.bool(), {"terminal_observation": self._term}
+
+    def step_raw(self, actions_u8):
+        """Launch one step; results land in self._obs/_rew/_done/_term.  No allocation, no sync."""
+        with torch.cuda.device(self.device):
+            nat.check(nat.load().futbol_step(self.ctx.h, actions_u8.data_ptr(), self._obs.data_ptr(),
+                                             self._rew.data_ptr(), self._done.data_ptr(), self._term.data_ptr(),
+                                             _stream_ptr(self.device)), self.ctx.h)
+
+    def random_actions(self, step, seed=1234, out=None):
+        """Synthetic policy (iid uniform actions, Philox tag-1 stream), written on device."""
+        out = self._act if out is None else out
+        with torch.cuda.device(self.device):
+            nat.check(nat.load().futbol_fill_actions(self.ctx.h, int(seed), int(step), out.data_ptr(),
+                                                     _stream_ptr(self.device)), self.ctx.h)
+        return out
+
+    def episode_stats(self, clear=False):
+        """Device f64[3] = [sum of finished-episode returns, #episodes, #env-steps] since last clear."""
+        with torch.cuda.device(self.device):
+            nat.check(nat.load().futbol_episode_stats(self.ctx.h, self._stats.data_ptr(), int(clear),
+                                                      _stream_ptr(self.device)), self.ctx.h)
+        return self._stats
+
+    def invalid_actions(self):
+        v = C.c_uint64()
+        with torch.cuda.device(self.device):
+            nat.check(nat.load().futbol_invalid_actions(self.ctx.h, C.byref(v), _stream_ptr(self.device)),
+                      self.ctx.h)
+        return v.value
+
+    # ------------------------------------------------------------ state I/O
+    def get_state(self):
+        """Host copy of the SoA state: {field: numpy array} (see csrc/futbol_state.hpp)."""
+        buf = np.zeros(self.ctx.state_bytes, dtype=np.uint8)
+        with torch.cuda.device(self.device):
+            nat.check(nat.load().futbol_get_state(self.ctx.h, buf.ctypes.data, 1, _stream_ptr(self.device)),
+                      self.ctx.h)
+        out = {}
+        for name, off, t, cnt in self.ctx.fields:
+            dt = np.dtype(_DT[t])
+            out[name] = buf[off:off + dt.itemsize * cnt].view(dt).copy()
+        return out
+
+    def set_state(self, state):
+        buf = np.zeros(self.ctx.state_bytes, dtype=np.uint8)
+        for name, off, t, cnt in self.ctx.fields:
+            dt = np.dtype(_DT[t])
+            a = np.ascontiguousarray(state[name], dtype=dt).reshape(-1)
+            if a.size != cnt:
+                raise ValueError("field %s: expected %d elements, got %d" % (name, cnt, a.size))
+            buf[off:off + dt.itemsize * cnt] = a.view(np.uint8)
+        with torch.cuda.device(self.device):
+            nat.check(nat.load().futbol_set_state(self.ctx.h, buf.ctypes.data, 1, _stream_ptr(self.device)),
+                      self.ctx.h)
+
+    def close(self):
+        if getattr(self, "ctx", None) is not None:
+            self.ctx.close()
+            self.ctx = None
+
+    # ------------------------------------------------ VecEnv-style plumbing
+    def step_async(self, actions):
+        self._pending = actions
+
+    def step_wait(self):
+        a, self._pending = self._pending, None
+        return self.step(a)
+
+    def seed(self, seed=None):
+        # env randomness is counter-based: re-seeding = a new context (see make())
+        return [self.seed_value + i for i in range(self.num_envs)]
+
+    def as_sb3(self):
+        return SB3VecEnv(self)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+try:  # pragma: no cover - stable-baselines3 is not installed in this image
+    from stable_baselines3.common.vec_env import VecEnv as _SB3Base  # type: ignore
+except Exception:  # noqa: BLE001
+    _SB3Base = object
+
+
+class SB3VecEnv(_SB3Base):
+    """stable-baselines VecEnv interface over a FutbolVecEnv (numpy in/out).
+
+    Rewards are float32 and obs are cast to the observation space dtype, as
+    DummyVecEnv does; infos carry `terminal_observation` for done envs and a
+    Monitor-style `episode` = {"r": return, "l": length}."""
+
+    def __init__(self, venv):
+        self.venv = venv
+        self.num_envs = venv.num_envs
+        self.observation_space = venv.observation_space
+        self.action_space = venv.action_space
+        self.metadata = {"render.modes": []}
+        self._actions = None
+        self._ep_ret = np.zeros(self.num_envs, np.float64)
+        self._ep_len = np.zeros(self.num_envs, np.int64)
+
+    def reset(self):
+        self._ep_ret[:] = 0
+        self._ep_len[:] = 0
+        return self.venv.reset().cpu().numpy().astype(self.observation_space.dtype)
+
+    def step_async(self, actions):
+        self._actions = np.asarray(actions)
+
+    def step_wait(self):
+        obs, rew, done, info = self.venv.step(self._actions)
+        obs_np = obs.cpu().numpy().astype(self.observation_space.dtype)
+        rew_np = rew.cpu().numpy().astype(np.float32)
+        done_np = done.cpu().numpy()
+        infos = [{} for _ in range(self.num_envs)]
+        self._ep_ret += rew.cpu().numpy().astype(np.float64)
+        self._ep_len += 1
+        if done_np.any():
+            term = info["terminal_observation"].cpu().numpy().astype(self.observation_space.dtype)
+            for i in np.nonzero(done_np)[0]:
+                infos[i]["terminal_observation"] = term[i]
+                infos[i]["episode"] = {"r": float(self._ep_ret[i]), "l": int(self._ep_len[i])}
+                self._ep_ret[i] = 0
+                self._ep_len[i] = 0
+        return obs_np, rew_np, done_np, infos
+
+    def step(self, actions):
+        self.step_async(actions)
+        return self.step_wait()
+
+    def close(self):
+        self.venv.close()
+
+    def seed(self, seed=None):
+        return self.venv.seed(seed)
+
+    def get_attr(self, attr_name, indices=None):
+        n = len(self._idx(indices))
+        return [getattr(self.venv, attr_name)] * n
+
+    def set_attr(self, attr_name, value, indices=None):
+        setattr(self.venv, attr_name, value)
+
+    def env_method(self, method_name, *args, indices=None, **kwargs):
+        return [getattr(self.venv, method_name)(*args, **kwargs)] * len(self._idx(indices))
+
+    def env_is_wrapped(self, wrapper_class, indices=None):
+        return [False] * len(self._idx(indices))
+
+    def get_images(self):
+        return []
+
+    def _idx(self, indices):
+        if indices is None:
+            return range(self.num_envs)
+        if isinstance(indices, int):
+            return [indices]
+        return indices

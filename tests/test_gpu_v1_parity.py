@@ -1,0 +1,166 @@
+"""envs_v1 kernel vs the CPU oracle, on the GPU.
+
+The kernel is compared BIT-FOR-BIT with oracle/liboracle_portable.so (the
+oracle with x*x squares, i.e. the kernel's arithmetic; see oracle/oracle_math.h):
+obs, reward, done, every body's p / v / v_bias and the arbiter cache, at every
+step of free-running rollouts with auto-reset, and on teacher-forced crowded
+states that exercise multi-contact solves, cached-impulse warm starts and the
+LDS->global contact spill.  North-star bar: bit-exact scoring/termination and
+<= 1e-5 on positions/velocities -- met here with 0 difference.
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import (O, v1_dense_cache, v1_oracle_bodies, v1_oracle_dense_cache, v1_oracle_to_state,
+                     v1_state_to_oracle)
+
+pytestmark = pytest.mark.gpu
+
+
+def _venv(n, B, seed, dtype=torch.float64, base=0):
+    from gym_futbol_amd import FutbolVecEnv
+    return FutbolVecEnv("v1", B, seed=seed, env_id_base=base, dtype=dtype, number_of_player=n)
+
+
+def _compare_state(venv, ora, n, B, tag):
+    st = venv.get_state()
+    ob = v1_oracle_bodies(ora.envs, n, B)
+    for f in ("px", "py", "vx", "vy", "bx", "by"):
+        d = np.abs(st[f] - ob[f]).max()
+        assert np.array_equal(st[f], ob[f]), "%s: %s differs (max %g)" % (tag, f, d)
+    ex, age, jn = v1_dense_cache(st, n, B)
+    ex2, age2, jn2 = v1_oracle_dense_cache(ora.envs, n, B)
+    assert np.array_equal(ex, ex2), tag + ": arbiter cache membership"
+    assert np.array_equal(age[ex], age2[ex2]), tag + ": arbiter ages"
+    assert np.array_equal(jn[ex], jn2[ex2]), tag + ": cached jnAcc"
+    meta = st["meta"].astype(np.uint64)
+    owner = (meta & np.uint64(7)).astype(np.int64)
+    assert np.array_equal(owner, np.array([ora.envs[i].owner for i in range(B)])), tag + ": ball_owner_side"
+    ev = (meta >> np.uint64(32)).astype(np.int64)
+    assert np.array_equal(ev, np.array([ora.envs[i].event for i in range(B)])), tag + ": rng event"
+
+
+@pytest.mark.parametrize("n,B,T", [(2, 1024, 620), (5, 256, 320), (10, 64, 320), (1, 128, 310), (3, 128, 310)])
+def test_free_running_rollout_bit_exact(n, B, T):
+    seed = 7 + n
+    venv = _venv(n, B, seed)
+    ora = O.V1Vec(B, N=n, seed=seed, portable=True)
+    _compare_state(venv, ora, n, B, "after create")
+    o_gpu = venv.reset().cpu().numpy()
+    o_cpu = ora.reset()
+    assert np.array_equal(o_gpu, o_cpu)
+    goals = dones = contacts = 0
+    for t in range(T):
+        a = venv.random_actions(t, seed=1234)
+        a_np = a.cpu().numpy().astype(np.int32)
+        obs, rew, done, info = venv.step(a)
+        o2, r2, d2, term2 = ora.step(a_np)
+        o1, r1, d1 = obs.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy()
+        assert np.array_equal(d1, d2), "done differs at step %d" % t
+        assert np.array_equal(r1, r2), "reward differs at step %d: max %g" % (t, np.abs(r1 - r2).max())
+        assert np.array_equal(o1, o2), "obs differs at step %d: max %g" % (t, np.abs(o1 - o2).max())
+        if d1.any():
+            assert np.array_equal(info["terminal_observation"].cpu().numpy()[d1], term2[d1])
+        goals += int((np.abs(r1) > 500).sum())
+        dones += int(d1.sum())
+        if t % 97 == 0:
+            _compare_state(venv, ora, n, B, "step %d" % t)
+            contacts += int((v1_dense_cache(venv.get_state(), n, B)[0]).sum())
+    _compare_state(venv, ora, n, B, "end")
+    # coverage: the rollout must have exercised goals, episode ends and contacts
+    assert dones >= B * (T // 300)
+    assert goals > 0 and contacts > 0
+    venv.close()
+
+
+def _crowded_states(n, B, seed):
+    """Oracle envs in random crowded configurations: bodies overlapping each other
+    and the walls / goal boxes, random v, v_bias and random cached arbiters."""
+    rng = np.random.default_rng(seed)
+    ora = O.V1Vec(B, N=n, seed=seed, portable=True)
+    nb = 2 * n + 1
+    P = nb * 12 + nb * (nb - 1) // 2
+    for i in range(B):
+        e = ora.envs[i]
+        mode = i % 4
+        for k in range(nb):
+            if mode == 0:  # cluster in the middle
+                x, y = 52.5 + rng.normal(0, 1.2), 34 + rng.normal(0, 1.2)
+            elif mode == 1:  # piled in a corner / goal mouth
+                x, y = rng.choice([0.3, 104.7]) + rng.normal(0, 1.0), rng.choice([1.0, 24.0, 44.0, 67.0]) + rng.normal(0, 1.0)
+            elif mode == 2:  # around the left goal box
+                x, y = -1.0 + rng.normal(0, 1.0), 34 + rng.normal(0, 8)
+            else:  # anywhere
+                x, y = rng.uniform(-3, 108), rng.uniform(-3, 71)
+            e.px[k], e.py[k] = x, y
+            e.vx[k], e.vy[k] = rng.normal(0, 6, 2)
+            e.bx[k], e.by[k] = rng.normal(0, 1, 2) * (rng.random() < 0.5)
+        e.stamp = 50
+        e.curr_dt = [0.1, 0.0001][int(rng.random() < 0.2)]
+        e.current_time = 0.0
+        for _ in range(int(rng.integers(0, 6))):
+            p = int(rng.integers(0, P))
+            age = int(rng.integers(0, 3))
+            e.arb_exists[p] = 1
+            e.arb_stamp[p] = e.stamp - age
+            e.arb_state[p] = 1 if age == 0 else 2
+            e.arb_inlist[p] = 1 if age == 0 else 0
+            e.arb_jn[p] = abs(rng.normal(0, 5))
+        e.owner = int(rng.integers(0, 2))
+        e.event = int(rng.integers(0, 1000))
+    return ora
+
+
+@pytest.mark.parametrize("n,B", [(2, 2048), (5, 512), (10, 128)])
+def test_teacher_forced_crowded_states(n, B):
+    seed = 100 + n
+    ora = _crowded_states(n, B, seed)
+    venv = _venv(n, B, seed)
+    st = v1_oracle_to_state(ora.envs, n, B)
+    venv.set_state(st)
+    # the oracle must see exactly the state the kernel got (stamps are relative)
+    v1_state_to_oracle(venv.get_state(), ora.envs, n, B)
+    for t in range(3):
+        a = venv.random_actions(900 + t, seed=4321)
+        obs, rew, done, _ = venv.step(a)
+        o2, r2, d2, _ = ora.step(a.cpu().numpy().astype(np.int32))
+        assert np.array_equal(done.cpu().numpy(), d2)
+        assert np.array_equal(rew.cpu().numpy(), r2), "step %d reward max diff %g" % (
+            t, np.abs(rew.cpu().numpy() - r2).max())
+        assert np.array_equal(obs.cpu().numpy(), o2), "step %d obs max diff %g" % (
+            t, np.abs(obs.cpu().numpy() - o2).max())
+        _compare_state(venv, ora, n, B, "crowded step %d" % t)
+    ex, _, _ = v1_dense_cache(venv.get_state(), n, B)
+    assert ex.sum(1).max() > 8, "crowded states must overflow the LDS contact slots"
+    venv.close()
+
+
+def test_float32_outputs_are_the_cast_of_float64():
+    B, n = 512, 2
+    a64, a32 = _venv(n, B, 3, torch.float64), _venv(n, B, 3, torch.float32)
+    o64, o32 = a64.reset(), a32.reset()
+    assert torch.equal(o64.float(), o32)
+    for t in range(310):
+        act = a64.random_actions(t)
+        r64 = a64.step(act)
+        r32 = a32.step(act)
+        assert torch.equal(r64[0].float(), r32[0]) and torch.equal(r64[1].float(), r32[1])
+        assert torch.equal(r64[2], r32[2])
+
+
+def test_sharding_invariance():
+    """An env's trajectory depends only on its global id, not on the shard it lives in."""
+    n, B = 2, 256
+    full = _venv(n, B, 11)
+    lo = _venv(n, B // 2, 11, base=0)
+    hi = _venv(n, B // 2, 11, base=B // 2)
+    f0 = full.reset()
+    assert torch.equal(f0, torch.cat([lo.reset(), hi.reset()]))
+    for t in range(320):
+        a = full.random_actions(t)
+        of, rf, df, _ = full.step(a)
+        ol, rl, dl, _ = lo.step(a[: B // 2].contiguous())
+        oh, rh, dh, _ = hi.step(a[B // 2:].contiguous())
+        assert torch.equal(of, torch.cat([ol, oh])) and torch.equal(rf, torch.cat([rl, rh]))
+        assert torch.equal(df, torch.cat([dl, dh]))
