@@ -66,6 +66,35 @@ def cpu_baseline(kind, n, budget_s=12.0, B=65536):
                       % ("envs_v1 2v2" if kind == "v1" else "v0 hard-coded-opponent", B, steps, dt)}
 
 
+STAMP_SLOTS = ["load state", "actions + opponent RNG", "process_action + out-of-bounds", "phase glue",
+               "integrate p + collide", "cache lookups + integrate v", "warm start + 10 solver iterations",
+               "arbiter cache update", "reward / goal / time", "goal reset + auto-reset phases", "obs + store"]
+
+
+def stamps_report(venv, one_step, args):
+    """Per-phase s_memtime breakdown of the step kernel (diagnostic build)."""
+    import ctypes as C
+    from gym_futbol_amd import _native as nat
+    nblk = (venv.num_envs + 63) // 64
+    buf = np.zeros((nblk + 1) * 16, np.uint64)
+    nat.check(nat.load().futbol_debug_stamps(venv.ctx.h, buf.ctypes.data, buf.size, 1), venv.ctx.h)
+    steps = args.steps
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one_step()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    nat.check(nat.load().futbol_debug_stamps(venv.ctx.h, buf.ctypes.data, buf.size, 0), venv.ctx.h)
+    epw = int(os.environ.get("FUTBOL_EPW", "64"))
+    per = buf[:nblk * 16].reshape(nblk, 16).astype(np.float64).sum(0) / (nblk * steps * (64 // epw))  # per wave
+    tot = per[:11].sum()
+    rep = {"diagnostic": "stamps", "envs_per_wave": epw, "steps": steps, "ms_per_step_wall": wall / steps * 1e3,
+           "cycles_per_wave_step_total": tot,
+           "phases": {STAMP_SLOTS[i]: {"cycles": per[i], "share": per[i] / tot} for i in range(11)}}
+    print(json.dumps(rep, indent=1))
+    venv.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -77,7 +106,11 @@ def main():
     ap.add_argument("--graph", type=int, default=1, help="replay the timed steps from a hipGraph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=200, help="steps timed per-kernel with HIP events")
+    ap.add_argument("--stamps", action="store_true",
+                    help="diagnostic: load the FUTBOL_STAMPS build and print the per-phase cycle breakdown")
     args = ap.parse_args()
+    if args.stamps:
+        os.environ["FUTBOL_LIB_VARIANT"] = "stamps"
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -118,6 +151,9 @@ def main():
         e1.record(stream)
     torch.cuda.synchronize(dev)
     kernel_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ev]))
+
+    if args.stamps:
+        return stamps_report(venv, one_step, args)
 
     graph = None
     G = 100

@@ -17,12 +17,15 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
-OBJ = os.path.join(HERE, "build", "obj")
-LIB = os.path.join(HERE, "gym_futbol_amd", "libfutbol_amd.so")
+VARIANT = os.environ.get("FUTBOL_BUILD_VARIANT", "")  # "stamps": diagnostic build with -DFUTBOL_STAMPS
+OBJ = os.path.join(HERE, "build", "obj" + ("_" + VARIANT if VARIANT else ""))
+LIB = os.path.join(HERE, "gym_futbol_amd", "libfutbol_amd%s.so" % ("_" + VARIANT if VARIANT else ""))
 ARCH = os.environ.get("FUTBOL_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fPIC",
           "-Wall", "-Wno-unused-function", "-I" + os.path.join(ROOT, "include")]
+if VARIANT == "stamps":
+    CFLAGS.append("-DFUTBOL_STAMPS")
 
 
 def _deps():

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <string>
 #include <vector>
@@ -34,6 +35,7 @@ struct FutbolCtx {
     int device = 0;
     uint64_t seed = 0, env_base = 0;
     int B = 0, N = 0, obs_dim = 0, act_dim = 0, K_done = 0;
+    int epw = 64;  // envs per one-wave block of the v1 kernels (FUTBOL_EPW=32 to override)
     void* d_params = nullptr;
     char* d_state = nullptr;
     size_t state_bytes = 0;
@@ -43,6 +45,7 @@ struct FutbolCtx {
     V1Ptrs v1{};
     V0Ptrs v0{};
     double steps_since_clear = 0.0;
+    unsigned long long* d_stamps = nullptr;  // diagnostic builds (FUTBOL_STAMPS) only
     std::string err;
 };
 
@@ -105,7 +108,30 @@ static void formation(int N, double W, double H, int side, int k, double* x, dou
     }
 }
 
-static void fill_v1_params(const FutbolConfig* c, uint64_t seed, uint64_t env_base, int B, int K_done, V1Params* p)
+// largest double s with RN(sqrt(s)) <= vmax: `sqrt(s) > vmax` <=> `s > T` (sqrt is correctly
+// rounded, hence monotone), which lets the kernel skip the sqrt of limit_velocity when no clamp happens
+static double clamp_threshold(double vmax)
+{
+    double s = vmax * vmax;
+    while (sqrt(s) > vmax) s = nextafter(s, 0.0);
+    while (sqrt(nextafter(s, INFINITY)) <= vmax) s = nextafter(s, INFINITY);
+    return s;
+}
+
+// the kernel's 16-bound candidate test must equal cpBBIntersects against every segment bb
+static bool bbt_consistent(const V1Params* p)
+{
+    const BBT& T = p->bbt;
+    const double L[12] = {T.lm1, T.lm1, T.lm1, T.lW1, T.lW1, T.lm1, T.lm3, T.lm3, T.lm3, T.lWp1, T.lW1, T.lW1};
+    const double Bo[12] = {T.bm1, T.bhi, T.bH, T.bm1, T.bhi, T.bm1, T.blo, T.blo, T.bhi, T.blo, T.blo, T.bhi};
+    const double R[12] = {T.r1, T.r1, T.rW1, T.rW1, T.rW1, T.rW1, T.rm1, T.r1, T.r1, T.rW3, T.rW3, T.rW3};
+    const double Tt[12] = {T.tlo, T.tH, T.tH, T.tlo, T.tH, T.t1, T.thi, T.tlo, T.thi, T.thi, T.tlo, T.thi};
+    for (int s = 0; s < 12; ++s)
+        if (L[s] != p->sl[s] || Bo[s] != p->sb[s] || R[s] != p->sr[s] || Tt[s] != p->st[s]) return false;
+    return true;
+}
+
+static int fill_v1_params(const FutbolConfig* c, uint64_t seed, uint64_t env_base, int B, int K_done, V1Params* p)
 {
     memset(p, 0, sizeof(*p));
     const double W = c->width, H = c->height, G = 20.0;  // GOAL_SIZE (envs_v1/futbol_env.py:21)
@@ -131,7 +157,16 @@ static void fill_v1_params(const FutbolConfig* c, uint64_t seed, uint64_t env_ba
         p->sb[s] = b - 1.0;
         p->sr[s] = r + 1.0;
         p->st[s] = t + 1.0;
+        const double sdx = seg[s][2] - seg[s][0], sdy = seg[s][3] - seg[s][1];
+        p->L2[s] = sdx * sdx + sdy * sdy;
+        p->rL2[s] = 1.0 / p->L2[s];
     }
+    // distinct BB bounds, segment by segment as used by the kernel's candidate test
+    BBT& T = p->bbt;
+    T.r1 = p->sr[0]; T.rW1 = p->sr[2]; T.rm1 = p->sr[6]; T.rW3 = p->sr[9];
+    T.lm1 = p->sl[0]; T.lW1 = p->sl[3]; T.lm3 = p->sl[6]; T.lWp1 = p->sl[9];
+    T.tlo = p->st[0]; T.tH = p->st[1]; T.t1 = p->st[5]; T.thi = p->st[6];
+    T.bm1 = p->sb[0]; T.bhi = p->sb[1]; T.bH = p->sb[2]; T.blo = p->sb[6];
     const int N = c->number_of_player;
     for (int side = 0; side < 2; ++side)
         for (int k = 0; k < N; ++k) formation(N, W, H, side, k, &p->fx[side * N + k], &p->fy[side * N + k]);
@@ -146,13 +181,17 @@ static void fill_v1_params(const FutbolConfig* c, uint64_t seed, uint64_t env_ba
     for (int i = 1; i < 3; ++i) {
         p->damp[i] = pow(0.95, p->dtv[i]);
         p->biasc[i] = 1.0 - pow(cbias, p->dtv[i]);
+        p->rdt[i] = 1.0 / p->dtv[i];
     }
     p->slop = (double)0.1f;
+    p->clamp2_player = clamp_threshold(10.0);  // PLAYER_MAX_VELOCITY
+    p->clamp2_ball = clamp_threshold(25.0);    // BALL_MAX_VELOCITY
     p->seed = seed;
     p->env_base = (uint32_t)env_base;
     p->B = B;
     p->K_done = K_done;
     p->auto_reset = c->auto_reset;
+    return bbt_consistent(p) ? 0 : -1;
 }
 
 // steps until `current_time += 0.1` (fp64, from 0) makes `current_time > total` (v1, :478-481)
@@ -295,7 +334,10 @@ extern "C" int futbol_create(const FutbolConfig* cfg, int32_t device, uint64_t s
         if ((he = hipMalloc((void**)&ctx->d_spill, slots * 8 * sizeof(double) * (size_t)B)) != hipSuccess)
             return bail(he, "hipMalloc(spill)");
         V1Params hp;
-        fill_v1_params(cfg, seed, env_id_base, B, ctx->K_done, &hp);
+        if (fill_v1_params(cfg, seed, env_id_base, B, ctx->K_done, &hp)) {
+            futbol_destroy(ctx);
+            return fail(nullptr, FUTBOL_EINVAL, "segment bounding boxes inconsistent (width/height)");
+        }
         if ((he = hipMalloc(&ctx->d_params, sizeof(V1Params))) != hipSuccess) return bail(he, "hipMalloc(params)");
         if ((he = hipMemcpy(ctx->d_params, &hp, sizeof(hp), hipMemcpyHostToDevice)) != hipSuccess)
             return bail(he, "hipMemcpy(params)");
@@ -315,8 +357,21 @@ extern "C" int futbol_create(const FutbolConfig* cfg, int32_t device, uint64_t s
         s.spill = ctx->d_spill;
         s.invalid = ctx->d_invalid;
         s.act_step = ctx->d_invalid + 1;
-        int rc = launch_v1(N, (const V1Params*)ctx->d_params, B, s, 0, 1, nullptr, nullptr, nullptr, nullptr,
-                           nullptr, nullptr, 1, 0);
+        s.stamps = nullptr;
+#ifdef FUTBOL_STAMPS
+        if ((he = hipMalloc((void**)&ctx->d_stamps, (size_t)((B + 63) / 64 + 1) * 16 * 8)) != hipSuccess)
+            return bail(he, "hipMalloc(stamps)");
+        if ((he = hipMemset(ctx->d_stamps, 0, (size_t)((B + 63) / 64) * 16 * 8)) != hipSuccess)
+            return bail(he, "hipMemset(stamps)");
+        s.stamps = ctx->d_stamps;
+#endif
+        if (const char* ev = getenv("FUTBOL_EPW")) ctx->epw = atoi(ev);
+        if (!v1_supported_epw(ctx->epw)) {
+            futbol_destroy(ctx);
+            return fail(nullptr, FUTBOL_EINVAL, "FUTBOL_EPW must be 64 or 32");
+        }
+        int rc = launch_v1(N, ctx->epw, (const V1Params*)ctx->d_params, B, s, 0, 1, nullptr, nullptr, nullptr,
+                           nullptr, nullptr, nullptr, 1, 0);
         if (rc) return bail(hipGetLastError(), "launch(init)");
     } else {
         V0Params hp;
@@ -351,6 +406,7 @@ extern "C" int futbol_destroy(FutbolCtx* ctx)
     if (ctx->d_spill) hipFree(ctx->d_spill);
     if (ctx->d_params) hipFree(ctx->d_params);
     if (ctx->d_invalid) hipFree(ctx->d_invalid);
+    if (ctx->d_stamps) hipFree(ctx->d_stamps);
     delete ctx;
     return FUTBOL_OK;
 }
@@ -383,8 +439,8 @@ static int launch(FutbolCtx* ctx, int what, const uint8_t* actions, const uint8_
     const int out64 = ctx->cfg.out_dtype == FUTBOL_F64;
     int rc;
     if (ctx->cfg.env_kind == FUTBOL_ENV_V1)
-        rc = launch_v1(ctx->N, (const V1Params*)ctx->d_params, ctx->B, ctx->v1, out64, what, actions, mask, obs,
-                       reward, done, term, 0, (hipStream_t)stream);
+        rc = launch_v1(ctx->N, ctx->epw, (const V1Params*)ctx->d_params, ctx->B, ctx->v1, out64, what, actions,
+                       mask, obs, reward, done, term, 0, (hipStream_t)stream);
     else
         rc = launch_v0((const V0Params*)ctx->d_params, ctx->B, ctx->v0, out64, what, actions, mask, obs, reward,
                        done, term, 0, (hipStream_t)stream);
@@ -485,5 +541,18 @@ extern "C" int futbol_set_state(FutbolCtx* ctx, const void* src, int32_t src_is_
                                      src_is_host ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice,
                                      (hipStream_t)stream));
     if (src_is_host) FB_CHECK_HIP(ctx, hipStreamSynchronize((hipStream_t)stream));
+    return FUTBOL_OK;
+}
+
+extern "C" int futbol_debug_stamps(FutbolCtx* ctx, uint64_t* host_out, int64_t n, int32_t clear)
+{
+    if (!ctx || !host_out) return FUTBOL_EINVAL;
+    if (!ctx->d_stamps) return fail(ctx, FUTBOL_EUNSUPPORTED, "not a FUTBOL_STAMPS diagnostic build / not v1");
+    const size_t bytes = (size_t)((ctx->B + 63) / 64) * 16 * 8;
+    if ((size_t)n * 8 < bytes) return fail(ctx, FUTBOL_EINVAL, "stamps buffer too small");
+    FB_CHECK_HIP(ctx, hipSetDevice(ctx->device));
+    FB_CHECK_HIP(ctx, hipDeviceSynchronize());
+    FB_CHECK_HIP(ctx, hipMemcpy(host_out, ctx->d_stamps, bytes, hipMemcpyDeviceToHost));
+    if (clear) FB_CHECK_HIP(ctx, hipMemset(ctx->d_stamps, 0, bytes));
     return FUTBOL_OK;
 }

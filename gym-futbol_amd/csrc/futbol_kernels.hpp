@@ -8,16 +8,29 @@
 
 namespace futbol {
 
+// The 16 distinct bounds of the 12 segment cpBBs (taken from sl/sb/sr/st): the
+// circle-vs-segment-BB test of segment s is  cl <= r_s && l_s <= cr && cb <= t_s && b_s <= ct.
+struct BBT {
+    double r1, rW1, rm1, rW3;   // r_s values
+    double lm1, lW1, lm3, lWp1; // l_s values
+    double tlo, tH, t1, thi;    // t_s values
+    double bm1, bhi, bH, blo;   // b_s values
+};
+
 // Per-context constants of an envs_v1 `Futbol` (kernel argument, < 2 KB).
 struct V1Params {
     double W, H;                                  // Futbol(width, height)
     double sax[12], say[12], sbx[12], sby[12];    // _setup_walls segments 0..11 (futbol_env.py:182-234)
     double sl[12], sb[12], sr[12], st[12];        // their cpBBs (radius 1 included)
+    BBT bbt;
     double fx[21], fy[21];                        // formation of bodies A.., B.., ball (team.py:52-112)
+    double L2[12], rL2[12];                       // |b - a|^2 of each segment and RN(1 / that)
     double dtv[3];                                // dt per dt code: {0, 1e-4, 0.1}
+    double rdt[3];                                // RN(1 / dt)
     double damp[3];                               // cpfpow(damping 0.95, dt)
     double biasc[3];                              // 1 - cpfpow(collisionBias, dt)
     double slop;                                  // collisionSlop (0.1f)
+    double clamp2_player, clamp2_ball;            // largest s with RN(sqrt(s)) <= vmax (limit_velocity)
     uint64_t seed;
     uint32_t env_base;                            // global id of env 0
     int B;
@@ -38,10 +51,11 @@ struct V0Params {
 };
 
 // P: device pointer to the context's V1Params (wave-uniform scalar loads)
-int launch_v1(int N, const V1Params* P, int B, const V1Ptrs& st, int out64, int what, const uint8_t* actions,
-              const uint8_t* mask, void* obs, void* reward, uint8_t* done, void* term, int init,
-              hipStream_t stream);
+int launch_v1(int N, int epw, const V1Params* P, int B, const V1Ptrs& st, int out64, int what,
+              const uint8_t* actions, const uint8_t* mask, void* obs, void* reward, uint8_t* done, void* term,
+              int init, hipStream_t stream);
 int v1_supported(int N);
+int v1_supported_epw(int epw);
 size_t v1_spill_slots(int N);
 
 int launch_v0(const V0Params* P, int B, const V0Ptrs& st, int out64, int what, const uint8_t* actions,

@@ -63,6 +63,7 @@ struct V1Ptrs {
     double* spill;        // contact records beyond the LDS capacity: [P][8][B]
     unsigned long long* invalid;  // count of clamped out-of-range actions
     unsigned long long* act_step; // synthetic-policy step counter, +1 per step launch
+    unsigned long long* stamps;   // diagnostic builds only (FUTBOL_STAMPS): [blocks][16] cycle sums
 };
 
 struct V0Ptrs {

@@ -8,20 +8,30 @@
 // other random choice from a counter-based Philox stream, and implements
 // DummyVecEnv's auto-reset in the same launch.
 //
-// Contacts: the narrowphase runs over all Nb*12 circle-segment and
-// Nb(Nb-1)/2 circle-circle pairs in the canonical order, with
-// exact broadphase rejections (cpBBIntersects, plus an "interior" test that
-// provably rejects all 12 segments at once).  Contact records go to LDS
-// (K slots per lane, lane-contiguous: conflict-free) and beyond K to a global
-// spill area, so there is no capacity limit.  During the sequential-impulse
-// solve the bodies' v / v_bias live in LDS too (per-lane dynamic indexing).
-// The persistent arbiter cache is a compact per-env list of (pair, age, jnAcc).
+// Exactness: -ffp-contract=off, only correctly rounded + - * / sqrt, and the
+// reference's operation order everywhere, so results are bit-identical to the
+// CPU oracle (tests/test_gpu_v1_parity.py).  Division by a constant c uses
+// q0 = x*rc, r = fma(-q0, c, x), q = fma(r, rc, q0) with rc = RN(1/c)
+// (Markstein's correction: correctly rounded, verified on 5.2e8 samples per
+// divisor, tests/test_gpu_numerics.py).
+//
+// Contacts: narrowphase over all Nb*12 circle-segment and Nb(Nb-1)/2
+// circle-circle pairs in the canonical order with exact
+// broadphase rejections (cpBBIntersects; an "interior" test that provably
+// rejects all 12 segments at once).  A body's candidate segments are
+// compacted into a per-lane bit mask and visited in ascending order, so a wave
+// iterates max-over-lanes candidates, not the union.  Contact records live in
+// LDS (K slots per lane, lane-contiguous: conflict-free) and beyond K in a
+// global spill area, so there is no capacity limit.  The sequential-impulse
+// solve keeps v / v_bias in LDS (double2, per-lane dynamic body index).  The
+// persistent arbiter cache is a compact per-env list of (pair, age, jnAcc);
+// its first CK entries are preloaded into registers with independent loads.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "futbol_kernels.hpp"
 #include "futbol_rng.hpp"
 #include "futbol_state.hpp"
-#include "futbol_kernels.hpp"
 #include "futbol_util.hpp"
 
 namespace futbol {
@@ -31,66 +41,184 @@ constexpr double kPlayerR = 1.5, kBallR = 1.0, kSegR = 1.0;
 constexpr double kPlayerMinv = 1.0 / 20.0, kBallMinv = 1.0 / 10.0;
 constexpr double kPlayerVmax = 10.0, kBallVmax = 25.0;
 constexpr double kE = 0.2;  // elasticity of players and ball; segments 0
+constexpr int CK = 4;       // arbiter-cache entries preloaded into registers
+
+// Diagnostic build only (-DFUTBOL_STAMPS, bench.py --stamps): per-wave s_memtime at phase
+// boundaries, accumulated into st.stamps[wave][slot].  Never compiled into the product.
+#ifdef FUTBOL_STAMPS
+#define FUTBOL_STAMP(slot)                                                                                \
+    do {                                                                                                  \
+        __builtin_amdgcn_s_waitcnt(0);                                                                    \
+        const unsigned long long _t = __builtin_amdgcn_s_memtime();                                      \
+        __builtin_amdgcn_s_waitcnt(0);                                                                    \
+        if ((threadIdx.x & 63) == 0 && st_stamps) {                                                       \
+            atomicAdd(&st_stamps[(size_t)(blockIdx.x * EPW / 64) * 16 + (slot)], _t - _stamp_prev);                            \
+        }                                                                                                 \
+        _stamp_prev = _t;                                                                                 \
+    } while (0)
+#else
+#define FUTBOL_STAMP(slot) do { } while (0)
+#endif
 
 template <int N>
 struct V1Shape {
     static constexpr int Nb = 2 * N + 1;
     static constexpr int BALL = 2 * N;
     static constexpr int P = v1_npairs(N);
-    // LDS slots per lane for contact records: 4 blocks (waves) per CU fit 160 KB
+    // LDS slots per lane for contact records: 4 one-wave blocks per CU fit in 160 KB
     static constexpr int K = N <= 2 ? 7 : (N <= 5 ? 4 : 2);
 };
 
-__device__ __forceinline__ double radius_of(int k, int ball) { return k == ball ? kBallR : kPlayerR; }
 __device__ __forceinline__ double minv_of(int k, int ball) { return k == ball ? kBallMinv : kPlayerMinv; }
 
-// contact record fields
-enum { F_NX = 0, F_NY, F_NMASS, F_BIAS, F_BOUNCE, F_JN, F_JB, F_NFIELDS };
+// correctly rounded x / c for a constant c with rc = RN(1/c)
+__device__ __forceinline__ double cdiv(double x, double c, double rc)
+{
+    const double q0 = x * rc;
+    const double r = __builtin_fma(-q0, c, x);
+    return __builtin_fma(r, rc, q0);
+}
 
-template <int N>
-struct Scratch {
-    using S = V1Shape<N>;
-    double rec[S::K][F_NFIELDS][64];
-    int info[S::K][64];
-    double vel[S::Nb][4][64];  // vx, vy, bx, by during the solve
+struct SegLds {
+    double ax, ay, sdx, sdy, L2, rL2;
 };
 
-template <int N>
-struct Lane {
+// EPW = envs (active lanes) per one-wave block.  Fewer than 64 leaves lanes idle but
+// puts several waves on each SIMD at B = 65536, which hides latency and balances
+// the per-wave work (the kernel ends with its slowest wave).
+template <int N, int EPW>
+struct Scratch {
     using S = V1Shape<N>;
-    Scratch<N>* sh;
-    double* spill;
-    uint16_t* ckey;
-    double* cjn;
-    int lane, env, B;
-
-    __device__ __forceinline__ double rget(int s, int f) const
-    {
-        if (s < S::K) return sh->rec[s][f][lane];
-        return spill[((size_t)(s - S::K) * 8 + f) * B + env];
-    }
-    __device__ __forceinline__ void rset(int s, int f, double v) const
-    {
-        if (s < S::K) sh->rec[s][f][lane] = v;
-        else spill[((size_t)(s - S::K) * 8 + f) * B + env] = v;
-    }
-    __device__ __forceinline__ int iget(int s) const
-    {
-        if (s < S::K) return sh->info[s][lane];
-        return (int)__double_as_longlong(spill[((size_t)(s - S::K) * 8 + 7) * B + env]);
-    }
-    __device__ __forceinline__ void iset(int s, int v) const
-    {
-        if (s < S::K) sh->info[s][lane] = v;
-        else spill[((size_t)(s - S::K) * 8 + 7) * B + env] = __longlong_as_double((long long)v);
-    }
-    __device__ __forceinline__ double& vel(int body, int c) const { return sh->vel[body][c][lane]; }
+    static constexpr int K = S::K * (64 / EPW);  // LDS contact slots per lane
+    // contact record s of lane l: rec[s][0][l] = (nx, ny), [1] = (nMass, bias),
+    // [2] = (bounce, info bits), [3] = (jnAcc, jBias): four ds_read_b128 per record
+    double2 rec[K][4][EPW];
+    double2 v[S::Nb][EPW];   // body velocity during the solve
+    double2 vb[S::Nb][EPW];  // body v_bias during the solve
+    SegLds seg[kNSeg];
 };
 
 // info word: a (5 bits) | bcode (6 bits: body id, or 32 + segment) << 5 | pair << 11 | normal << 20
 __device__ __forceinline__ int pack_info(int a, int bcode, int pair, bool normal)
 {
     return a | (bcode << 5) | (pair << 11) | ((normal ? 1 : 0) << 20);
+}
+
+// global spill record (slot s >= K): 8 doubles [nx, ny, nMass, bias, bounce, info, jnAcc, jBias]
+template <int N, int EPW>
+struct Lane {
+    using S = V1Shape<N>;
+    static constexpr int KL = Scratch<N, EPW>::K;
+    Scratch<N, EPW>* sh;
+    double* spill;
+    uint16_t* ckey;
+    double* cjn;
+    int lane, env, B;
+
+    __device__ __forceinline__ double* sp(int s, int f) const { return spill + ((size_t)(s - KL) * 8 + f) * B + env; }
+    // record s as 4 double2 (any slot)
+    __device__ __forceinline__ double2 get(int s, int q) const
+    {
+        if (s < KL) return sh->rec[s][q][lane];
+        return make_double2(*sp(s, 2 * q), *sp(s, 2 * q + 1));
+    }
+    __device__ __forceinline__ void put(int s, int q, double2 x) const
+    {
+        if (s < KL) sh->rec[s][q][lane] = x;
+        else {
+            *sp(s, 2 * q) = x.x;
+            *sp(s, 2 * q + 1) = x.y;
+        }
+    }
+    __device__ __forceinline__ int get_info(int s) const { return (int)__double_as_longlong(get(s, 2).y); }
+    __device__ __forceinline__ double get_jn(int s) const { return get(s, 3).x; }
+    __device__ __forceinline__ void set_rec(int s, double nx, double ny, double nm, double bi, double bo, double j,
+                                            int info) const
+    {
+        put(s, 0, make_double2(nx, ny));
+        put(s, 1, make_double2(nm, bi));
+        put(s, 2, make_double2(bo, __longlong_as_double((long long)info)));
+        put(s, 3, make_double2(j, 0.0));
+    }
+};
+
+// One contact of cpArbiterApplyImpulse (frictionless), record and body velocities in
+// LDS (FAST: slot < K, no branches) or the record in the global spill area.
+template <int N, int EPW, bool FAST>
+__device__ __forceinline__ void solve_contact(const Lane<N, EPW>& L, int s)
+{
+    using S = V1Shape<N>;
+    Scratch<N, EPW>* sh = L.sh;
+    const int ln = L.lane;
+    double2 r0, r1, r2, r3;
+    if constexpr (FAST) {
+        r0 = sh->rec[s][0][ln];
+        r1 = sh->rec[s][1][ln];
+        r2 = sh->rec[s][2][ln];
+        r3 = sh->rec[s][3][ln];
+    } else {
+        r0 = L.get(s, 0);
+        r1 = L.get(s, 1);
+        r2 = L.get(s, 2);
+        r3 = L.get(s, 3);
+    }
+    const int info = (int)__double_as_longlong(r2.y);
+    const int a = info & 31, bcode = (info >> 5) & 63;
+    const bool dyn = bcode < 32;
+    const int b = dyn ? bcode : a;  // any valid slot; masked by dyn below
+    const double nx = r0.x, ny = r0.y, nMass = r1.x, bias = r1.y, bounce = r2.x;
+    const double jnOld = r3.x, jbOld = r3.y;
+    const double2 va = sh->v[a][ln], ba = sh->vb[a][ln];
+    double2 vbv = sh->v[b][ln], bbv = sh->vb[b][ln];
+    if (!dyn) {
+        vbv = make_double2(0.0, 0.0);
+        bbv = make_double2(0.0, 0.0);
+    }
+    const double vbn = (bbv.x - ba.x) * nx + (bbv.y - ba.y) * ny;
+    const double vrn = (vbv.x - va.x) * nx + (vbv.y - va.y) * ny;
+    const double jbn = (bias - vbn) * nMass;
+    const double tb = jbOld + jbn;
+    const double jb = tb > 0.0 ? tb : 0.0;
+    const double jnv = -(bounce + vrn) * nMass;
+    const double tn = jnOld + jnv;
+    const double jnAcc = tn > 0.0 ? tn : 0.0;
+    if constexpr (FAST) sh->rec[s][3][ln] = make_double2(jnAcc, jb);
+    else L.put(s, 3, make_double2(jnAcc, jb));
+    const double db = jb - jbOld, dj = jnAcc - jnOld;
+    const double jbx = nx * db, jby = ny * db, jx = nx * dj, jy = ny * dj;
+    const double ma = minv_of(a, S::BALL);
+    sh->vb[a][ln] = make_double2(ba.x + (-jbx) * ma, ba.y + (-jby) * ma);
+    sh->v[a][ln] = make_double2(va.x + (-jx) * ma, va.y + (-jy) * ma);
+    if (dyn) {
+        const double mb = minv_of(b, S::BALL);
+        sh->vb[b][ln] = make_double2(bbv.x + jbx * mb, bbv.y + jby * mb);
+        sh->v[b][ln] = make_double2(vbv.x + jx * mb, vbv.y + jy * mb);
+    }
+}
+
+// cpArbiterApplyCachedImpulse for one contact (only NORMAL arbiters are warm started)
+template <int N, int EPW, bool FAST>
+__device__ __forceinline__ void warm_contact(const Lane<N, EPW>& L, int s, double dt_coef)
+{
+    using S = V1Shape<N>;
+    Scratch<N, EPW>* sh = L.sh;
+    const int ln = L.lane;
+    const double2 r0 = FAST ? sh->rec[s][0][ln] : L.get(s, 0);
+    const double2 r2 = FAST ? sh->rec[s][2][ln] : L.get(s, 2);
+    const double2 r3 = FAST ? sh->rec[s][3][ln] : L.get(s, 3);
+    const int info = (int)__double_as_longlong(r2.y);
+    if (!((info >> 20) & 1)) return;
+    const int a = info & 31, bcode = (info >> 5) & 63;
+    const double jn = r3.x;
+    const double jx = (r0.x * jn) * dt_coef, jy = (r0.y * jn) * dt_coef;
+    const double ma = minv_of(a, S::BALL);
+    const double2 va = sh->v[a][ln];
+    sh->v[a][ln] = make_double2(va.x + (-jx) * ma, va.y + (-jy) * ma);
+    if (bcode < 32) {
+        const double mb = minv_of(bcode, S::BALL);
+        const double2 vbb = sh->v[bcode][ln];
+        sh->v[bcode][ln] = make_double2(vbb.x + jx * mb, vbb.y + jy * mb);
+    }
 }
 
 template <int N>
@@ -133,14 +261,21 @@ __device__ __forceinline__ bool cc_hit(double ax, double ay, double ra, double b
     return dx * dx + dy * dy < mind * mind;
 }
 
-__device__ __forceinline__ bool cs_test(double cx, double cy, double rc, double sax, double say, double sbx,
-                                        double sby, double& nx, double& ny, double& p1x, double& p1y,
-                                        double& p2x, double& p2y)
+// closest point of segment (sa, sa + sd) to c; t = dot(sd, c - sa) / |sd|^2 clamped
+__device__ __forceinline__ void seg_closest(double cx, double cy, double sax, double say, double sdx, double sdy,
+                                            double L2, double rL2, double& qx, double& qy)
 {
-    const double sdx = sbx - sax, sdy = sby - say;
-    double t = (sdx * (cx - sax) + sdy * (cy - say)) / (sdx * sdx + sdy * sdy);
+    double t = cdiv(sdx * (cx - sax) + sdy * (cy - say), L2, rL2);
     t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
-    const double qx = sax + sdx * t, qy = say + sdy * t;
+    qx = sax + sdx * t;
+    qy = say + sdy * t;
+}
+
+__device__ __forceinline__ bool cs_test(double cx, double cy, double rc, const SegLds& g, double& nx, double& ny,
+                                        double& p1x, double& p1y, double& p2x, double& p2y)
+{
+    double qx, qy;
+    seg_closest(cx, cy, g.ax, g.ay, g.sdx, g.sdy, g.L2, g.rL2, qx, qy);
     const double mind = rc + kSegR;
     const double dx = qx - cx, dy = qy - cy;
     const double d2 = dx * dx + dy * dy;
@@ -150,10 +285,10 @@ __device__ __forceinline__ bool cs_test(double cx, double cy, double rc, double 
         const double inv = 1.0 / d;
         nx = dx * inv;
         ny = dy * inv;
-    } else {
-        const double inv = 1.0 / sqrt(sdx * sdx + sdy * sdy);
-        nx = -sdy * inv;
-        ny = sdx * inv;
+    } else {  // segment->tn
+        const double inv = 1.0 / sqrt(g.L2);
+        nx = -g.sdy * inv;
+        ny = g.sdx * inv;
     }
     p1x = cx + nx * rc;
     p1y = cy + ny * rc;
@@ -162,13 +297,11 @@ __device__ __forceinline__ bool cs_test(double cx, double cy, double rc, double 
     return true;
 }
 
-__device__ __forceinline__ bool cs_hit(double cx, double cy, double rc, double sax, double say, double sbx,
-                                       double sby)
+__device__ __forceinline__ bool cs_hit(const V1Params* __restrict__ P, int s, double cx, double cy, double rc)
 {
-    const double sdx = sbx - sax, sdy = sby - say;
-    double t = (sdx * (cx - sax) + sdy * (cy - say)) / (sdx * sdx + sdy * sdy);
-    t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
-    const double qx = sax + sdx * t, qy = say + sdy * t;
+    double qx, qy;
+    seg_closest(cx, cy, P->sax[s], P->say[s], P->sbx[s] - P->sax[s], P->sby[s] - P->say[s], P->L2[s], P->rL2[s],
+                qx, qy);
     const double mind = rc + kSegR;
     const double dx = qx - cx, dy = qy - cy;
     return dx * dx + dy * dy < mind * mind;
@@ -182,40 +315,17 @@ __device__ __forceinline__ bool far_from_segments(double x, double y, double rea
 }
 
 // ---------------------------------------------------------------------------
-// preStep of one new contact (cpArbiterPreStep), written to contact slot n.
-// Called with the bodies' values already loaded (no per-lane array indexing).
-template <int N>
-__device__ __forceinline__ void record_contact(const Lane<N>& L, int n, int info, double biasCoef, double dt,
-                                               double slop, double nx, double ny, double p1x, double p1y,
-                                               double p2x, double p2y, double apx, double apy, double avx,
-                                               double avy, double ma, double bpx, double bpy, double bvx_,
-                                               double bvy_, double mb, double ee)
-{
-    const double r1x = p1x - apx, r1y = p1y - apy;
-    const double r2x = p2x - bpx, r2y = p2y - bpy;
-    const double nMass = 1.0 / (ma + mb);
-    const double bdx = bpx - apx, bdy = bpy - apy;
-    const double dist = ((r2x - r1x) + bdx) * nx + ((r2y - r1y) + bdy) * ny;
-    double m = dist + slop;
-    m = (0.0 < m) ? 0.0 : m;
-    const double bias = -biasCoef * m / dt;
-    const double bounce = ((bvx_ - avx) * nx + (bvy_ - avy) * ny) * ee;
-    L.rset(n, F_NX, nx);
-    L.rset(n, F_NY, ny);
-    L.rset(n, F_NMASS, nMass);
-    L.rset(n, F_BIAS, bias);
-    L.rset(n, F_BOUNCE, bounce);
-    L.rset(n, F_JN, 0.0);
-    L.rset(n, F_JB, 0.0);
-    L.iset(n, info);
-}
-
 // cpSpaceStep(dt) for one env.  dtc: 1 -> 1e-4, 2 -> 0.1
-template <int N>
-__device__ __forceinline__ void space_step(const V1Params* __restrict__ P, const Lane<N>& L, Env<N>& e, int dtc)
+template <int N, int EPW>
+__device__ __forceinline__ void space_step(const V1Params* __restrict__ P, const Lane<N, EPW>& L, Env<N>& e, int dtc
+#ifdef FUTBOL_STAMPS
+                                           , unsigned long long* st_stamps, unsigned long long& _stamp_prev
+#endif
+)
 {
     using S = V1Shape<N>;
     const double dt = dtc == 2 ? P->dtv[2] : P->dtv[1];
+    const double rdt = dtc == 2 ? P->rdt[2] : P->rdt[1];
     const uint32_t pc = e.meta.dtcode();
     const double prev_dt = pc == 2 ? P->dtv[2] : (pc == 1 ? P->dtv[1] : 0.0);
     const double biasCoef = dtc == 2 ? P->biasc[2] : P->biasc[1];
@@ -224,6 +334,20 @@ __device__ __forceinline__ void space_step(const V1Params* __restrict__ P, const
     e.meta.set_dtcode(dtc);
     const int B = L.B, env = L.env;
     const uint32_t ncache = e.meta.ncache();
+
+    // arbiter cache: first CK entries into registers, with independent loads
+    uint32_t ck[CK];
+    double cj[CK];
+#pragma unroll
+    for (int c = 0; c < CK; ++c) {
+        ck[c] = 0xffffu;
+        cj[c] = 0.0;
+        if ((uint32_t)c < ncache) {
+            ck[c] = L.ckey[(size_t)c * B + env];
+            cj[c] = L.cjn[(size_t)c * B + env];
+        }
+    }
+    uint32_t touched = 0;  // preloaded entries matched by this step's contacts
 
     // cpBodyUpdatePosition
     sfor<S::Nb>([&](auto K) {
@@ -234,8 +358,33 @@ __device__ __forceinline__ void space_step(const V1Params* __restrict__ P, const
         e.by[k] = 0.0;
     });
 
-    // collide in canonical order, preStep folded in (it needs pre-damping v)
+    // collide in canonical order; cpArbiterUpdate + preStep folded in (needs pre-damping v)
     int n = 0;
+    auto record = [&](int a, int bcode, int pair, double nx, double ny, double p1x, double p1y, double p2x,
+                      double p2y, double apx, double apy, double avx, double avy, double ma, double bpx, double bpy,
+                      double bvx_, double bvy_, double mb, double ee) {
+        const double r1x = p1x - apx, r1y = p1y - apy;
+        const double r2x = p2x - bpx, r2y = p2y - bpy;
+        const double nMass = 1.0 / (ma + mb);
+        const double bdx = bpx - apx, bdy = bpy - apy;
+        const double dist = ((r2x - r1x) + bdx) * nx + ((r2y - r1y) + bdy) * ny;
+        double m = dist + slop;
+        m = (0.0 < m) ? 0.0 : m;
+        const double bias = cdiv(-biasCoef * m, dt, rdt);
+        const double bounce = ((bvx_ - avx) * nx + (bvy_ - avy) * ny) * ee;
+        double jn = 0.0;
+        bool normal = false;
+#pragma unroll
+        for (int c = 0; c < CK; ++c)
+            if ((int)(ck[c] & 0x3ffu) == pair) {
+                jn = cj[c];
+                normal = (ck[c] >> 12) == 0;  // touched by the previous step: NORMAL -> warm start
+                touched |= 1u << c;
+            }
+        L.set_rec(n, nx, ny, nMass, bias, bounce, jn, pack_info(a, bcode, pair, normal));
+        ++n;
+    };
+
     sfor<S::Nb>([&](auto I) {
         constexpr int i = I;
         constexpr double ri = i == S::BALL ? kBallR : kPlayerR;
@@ -244,16 +393,33 @@ __device__ __forceinline__ void space_step(const V1Params* __restrict__ P, const
         // every segment's cpBB lies within 1 of the field border: exact reject of all 12
         const bool interior = cl > 1.0 && cr < W - 1.0 && cb > 1.0 && ct < H - 1.0;
         if (!interior) {
-            for (int s = 0; s < kNSeg; ++s) {  // wave-uniform s: scalar loads of the geometry
-                if (!(cl <= P->sr[s] && P->sl[s] <= cr && cb <= P->st[s] && P->sb[s] <= ct)) continue;
+            // cpBBIntersects(circle, segment s) for all 12 segments from the 16 distinct bounds
+            const BBT& T = P->bbt;
+            const bool r1 = cl <= T.r1, rW1 = cl <= T.rW1, rm1 = cl <= T.rm1, rW3 = cl <= T.rW3;
+            const bool lm1 = T.lm1 <= cr, lW1 = T.lW1 <= cr, lm3 = T.lm3 <= cr, lWp1 = T.lWp1 <= cr;
+            const bool tlo = cb <= T.tlo, tH = cb <= T.tH, t1 = cb <= T.t1, thi = cb <= T.thi;
+            const bool bm1 = T.bm1 <= ct, bhi = T.bhi <= ct, bH = T.bH <= ct, blo = T.blo <= ct;
+            uint32_t cand = 0;
+            cand |= (r1 && lm1 && tlo && bm1) ? 1u << 0 : 0u;
+            cand |= (r1 && lm1 && tH && bhi) ? 1u << 1 : 0u;
+            cand |= (rW1 && lm1 && tH && bH) ? 1u << 2 : 0u;
+            cand |= (rW1 && lW1 && tlo && bm1) ? 1u << 3 : 0u;
+            cand |= (rW1 && lW1 && tH && bhi) ? 1u << 4 : 0u;
+            cand |= (rW1 && lm1 && t1 && bm1) ? 1u << 5 : 0u;
+            cand |= (rm1 && lm3 && thi && blo) ? 1u << 6 : 0u;
+            cand |= (r1 && lm3 && tlo && blo) ? 1u << 7 : 0u;
+            cand |= (r1 && lm3 && thi && bhi) ? 1u << 8 : 0u;
+            cand |= (rW3 && lWp1 && thi && blo) ? 1u << 9 : 0u;
+            cand |= (rW3 && lW1 && tlo && blo) ? 1u << 10 : 0u;
+            cand |= (rW3 && lW1 && thi && bhi) ? 1u << 11 : 0u;
+            while (cand) {  // ascending segment order, per-lane trip count
+                const int s = __builtin_ctz(cand);
+                cand &= cand - 1;
+                const SegLds g = L.sh->seg[s];
                 double nx, ny, p1x, p1y, p2x, p2y;
-                if (cs_test(e.px[i], e.py[i], ri, P->sax[s], P->say[s], P->sbx[s], P->sby[s], nx, ny, p1x, p1y,
-                            p2x, p2y)) {
-                    record_contact<N>(L, n, pack_info(i, 32 + s, i * kNSeg + s, false), biasCoef, dt, slop, nx,
-                                      ny, p1x, p1y, p2x, p2y, e.px[i], e.py[i], e.vx[i], e.vy[i], mi, 0.0, 0.0,
-                                      0.0, 0.0, 0.0, kE * 0.0);
-                    ++n;
-                }
+                if (cs_test(e.px[i], e.py[i], ri, g, nx, ny, p1x, p1y, p2x, p2y))
+                    record(i, 32 + s, i * kNSeg + s, nx, ny, p1x, p1y, p2x, p2y, e.px[i], e.py[i], e.vx[i], e.vy[i],
+                           mi, 0.0, 0.0, 0.0, 0.0, 0.0, kE * 0.0);
             }
         }
         sfor<i + 1, S::Nb>([&](auto J) {
@@ -264,137 +430,112 @@ __device__ __forceinline__ void space_step(const V1Params* __restrict__ P, const
             double nx, ny, p1x, p1y, p2x, p2y;
             if (cc_test(e.px[i], e.py[i], ri, e.px[j], e.py[j], rj, nx, ny, p1x, p1y, p2x, p2y)) {
                 constexpr int pair = S::Nb * kNSeg + i * S::Nb - i * (i + 1) / 2 + (j - i - 1);
-                record_contact<N>(L, n, pack_info(i, j, pair, false), biasCoef, dt, slop, nx, ny, p1x, p1y, p2x,
-                                  p2y, e.px[i], e.py[i], e.vx[i], e.vy[i], mi, e.px[j], e.py[j], e.vx[j],
-                                  e.vy[j], mj, kE * kE);
-                ++n;
+                record(i, j, pair, nx, ny, p1x, p1y, p2x, p2y, e.px[i], e.py[i], e.vx[i], e.vy[i], mi, e.px[j],
+                       e.py[j], e.vx[j], e.vy[j], mj, kE * kE);
             }
         });
     });
 
-    // arbiter cache lookup (cpArbiterUpdate copies the old contact's jnAcc;
-    // an arbiter touched by the previous step is NORMAL -> warm started)
-    for (int s = 0; s < n; ++s) {
-        const int info = L.iget(s);
-        const int pair = (info >> 11) & 511;
-        for (uint32_t c = 0; c < ncache; ++c) {
-            const uint32_t key = L.ckey[(size_t)c * B + env];
-            if ((int)(key & 0x3ffu) == pair) {
-                L.rset(s, F_JN, L.cjn[(size_t)c * B + env]);
-                if ((key >> 12) == 0) L.iset(s, info | (1 << 20));
-                break;
+    FUTBOL_STAMP(dtc == 2 ? 4 : 9);
+    // cache entries beyond the preloaded ones (rare): look them up in global memory
+    if (ncache > (uint32_t)CK) {
+        for (int s = 0; s < n; ++s) {
+            const int info = L.get_info(s);
+            const int pair = (info >> 11) & 511;
+            bool pre = false;
+#pragma unroll
+            for (int c = 0; c < CK; ++c) pre |= (int)(ck[c] & 0x3ffu) == pair;
+            if (pre) continue;
+            for (uint32_t c = CK; c < ncache; ++c) {
+                const uint32_t key = L.ckey[(size_t)c * B + env];
+                if ((int)(key & 0x3ffu) == pair) {
+                    const double2 r2 = L.get(s, 2);
+                    L.put(s, 3, make_double2(L.cjn[(size_t)c * B + env], 0.0));
+                    if ((key >> 12) == 0)
+                        L.put(s, 2, make_double2(r2.x, __longlong_as_double((long long)(info | (1 << 20)))));
+                    break;
+                }
             }
         }
     }
 
-    // cpBodyUpdateVelocity + the reference's limit_velocity callback
+    // cpBodyUpdateVelocity + the reference's limit_velocity callback:
+    // sqrt(vx^2+vy^2) > vmax  <=>  vx^2+vy^2 > T (T = largest double whose rounded sqrt is <= vmax)
     sfor<S::Nb>([&](auto K) {
         constexpr int k = K;
         e.vx[k] = e.vx[k] * damping + 0.0 * dt;
         e.vy[k] = e.vy[k] * damping + 0.0 * dt;
-        const double l = sqrt(e.vx[k] * e.vx[k] + e.vy[k] * e.vy[k]);
-        constexpr double vmax = k == S::BALL ? kBallVmax : kPlayerVmax;
-        if (l > vmax) {
-            const double sc = vmax / l;
+        const double s2 = e.vx[k] * e.vx[k] + e.vy[k] * e.vy[k];
+        const double thr = k == S::BALL ? P->clamp2_ball : P->clamp2_player;
+        if (s2 > thr) {
+            constexpr double vmax = k == S::BALL ? kBallVmax : kPlayerVmax;
+            const double sc = vmax / sqrt(s2);
             e.vx[k] = e.vx[k] * sc;
             e.vy[k] = e.vy[k] * sc;
         }
     });
 
+    FUTBOL_STAMP(dtc == 2 ? 5 : 9);
     if (n > 0) {
+        Scratch<N, EPW>* sh = L.sh;
+        const int ln = L.lane;
         sfor<S::Nb>([&](auto K) {
             constexpr int k = K;
-            L.vel(k, 0) = e.vx[k];
-            L.vel(k, 1) = e.vy[k];
-            L.vel(k, 2) = 0.0;
-            L.vel(k, 3) = 0.0;
+            sh->v[k][ln] = make_double2(e.vx[k], e.vy[k]);
+            sh->vb[k][ln] = make_double2(0.0, 0.0);
         });
-        // cpArbiterApplyCachedImpulse
+        constexpr int KL = Lane<N, EPW>::KL;
+        const int nf = n < KL ? n : KL;  // records in LDS; slots >= KL are in the global spill
         const double dt_coef = (prev_dt == 0.0) ? 0.0 : dt / prev_dt;
-        for (int s = 0; s < n; ++s) {
-            const int info = L.iget(s);
-            if (!((info >> 20) & 1)) continue;
-            const int a = info & 31, bcode = (info >> 5) & 63;
-            const double nx = L.rget(s, F_NX), ny = L.rget(s, F_NY), jn = L.rget(s, F_JN);
-            const double jx = (nx * jn) * dt_coef, jy = (ny * jn) * dt_coef;
-            const double ma = minv_of(a, S::BALL);
-            L.vel(a, 0) = L.vel(a, 0) + (-jx) * ma;
-            L.vel(a, 1) = L.vel(a, 1) + (-jy) * ma;
-            if (bcode < 32) {
-                const double mb = minv_of(bcode, S::BALL);
-                L.vel(bcode, 0) = L.vel(bcode, 0) + jx * mb;
-                L.vel(bcode, 1) = L.vel(bcode, 1) + jy * mb;
-            }
-        }
-        // cpArbiterApplyImpulse x 10 (frictionless: u = 0)
+        for (int s = 0; s < nf; ++s) warm_contact<N, EPW, true>(L, s, dt_coef);
+        for (int s = KL; s < n; ++s) warm_contact<N, EPW, false>(L, s, dt_coef);
         for (int it = 0; it < 10; ++it) {
-            for (int s = 0; s < n; ++s) {
-                const int info = L.iget(s);
-                const int a = info & 31, bcode = (info >> 5) & 63;
-                const bool dyn = bcode < 32;
-                const int bb = dyn ? bcode : a;  // any valid slot; masked by dyn below
-                const double nx = L.rget(s, F_NX), ny = L.rget(s, F_NY);
-                const double nMass = L.rget(s, F_NMASS);
-                const double avx = L.vel(a, 0), avy = L.vel(a, 1), abx = L.vel(a, 2), aby = L.vel(a, 3);
-                const double bvx_ = dyn ? L.vel(bb, 0) : 0.0, bvy_ = dyn ? L.vel(bb, 1) : 0.0;
-                const double bbx_ = dyn ? L.vel(bb, 2) : 0.0, bby_ = dyn ? L.vel(bb, 3) : 0.0;
-                const double vbn = (bbx_ - abx) * nx + (bby_ - aby) * ny;
-                const double vrn = (bvx_ - avx) * nx + (bvy_ - avy) * ny;
-                const double jbn = (L.rget(s, F_BIAS) - vbn) * nMass;
-                const double jbOld = L.rget(s, F_JB);
-                const double tb = jbOld + jbn;
-                const double jb = tb > 0.0 ? tb : 0.0;
-                const double jnv = -(L.rget(s, F_BOUNCE) + vrn) * nMass;
-                const double jnOld = L.rget(s, F_JN);
-                const double tn = jnOld + jnv;
-                const double jnAcc = tn > 0.0 ? tn : 0.0;
-                L.rset(s, F_JB, jb);
-                L.rset(s, F_JN, jnAcc);
-                const double db = jb - jbOld, dj = jnAcc - jnOld;
-                const double jbx = nx * db, jby = ny * db, jx = nx * dj, jy = ny * dj;
-                const double ma = minv_of(a, S::BALL);
-                L.vel(a, 2) = abx + (-jbx) * ma;
-                L.vel(a, 3) = aby + (-jby) * ma;
-                L.vel(a, 0) = avx + (-jx) * ma;
-                L.vel(a, 1) = avy + (-jy) * ma;
-                if (dyn) {
-                    const double mb = minv_of(bb, S::BALL);
-                    L.vel(bb, 2) = bbx_ + jbx * mb;
-                    L.vel(bb, 3) = bby_ + jby * mb;
-                    L.vel(bb, 0) = bvx_ + jx * mb;
-                    L.vel(bb, 1) = bvy_ + jy * mb;
-                }
-            }
+            for (int s = 0; s < nf; ++s) solve_contact<N, EPW, true>(L, s);
+            for (int s = KL; s < n; ++s) solve_contact<N, EPW, false>(L, s);
         }
         sfor<S::Nb>([&](auto K) {
             constexpr int k = K;
-            e.vx[k] = L.vel(k, 0);
-            e.vy[k] = L.vel(k, 1);
-            e.bx[k] = L.vel(k, 2);
-            e.by[k] = L.vel(k, 3);
+            const double2 v = sh->v[k][ln], vb = sh->vb[k][ln];
+            e.vx[k] = v.x;
+            e.vy[k] = v.y;
+            e.bx[k] = vb.x;
+            e.by[k] = vb.y;
         });
     }
 
+    FUTBOL_STAMP(dtc == 2 ? 6 : 9);
     // cpSpaceArbiterSetFilter + store jnAcc: survivors (untouched, age+1 < 3) then this step's contacts
     uint32_t w = 0;
-    for (uint32_t c = 0; c < ncache; ++c) {
+#pragma unroll
+    for (int c = 0; c < CK; ++c) {
+        if ((uint32_t)c < ncache) {
+            const uint32_t key = ck[c], age = key >> 12;
+            if (!((touched >> c) & 1u) && age + 1 < 3) {
+                L.ckey[(size_t)w * B + env] = (uint16_t)((key & 0x3ffu) | ((age + 1) << 12));
+                L.cjn[(size_t)w * B + env] = cj[c];
+                ++w;
+            }
+        }
+    }
+    for (uint32_t c = CK; c < ncache; ++c) {
         const uint32_t key = L.ckey[(size_t)c * B + env];
         const int pair = (int)(key & 0x3ffu);
         const uint32_t age = key >> 12;
-        bool touched = false;
-        for (int s = 0; s < n; ++s) touched |= ((L.iget(s) >> 11) & 511) == pair;
-        if (!touched && age + 1 < 3) {
-            if (w != c) L.cjn[(size_t)w * B + env] = L.cjn[(size_t)c * B + env];
+        bool t = false;
+        for (int s = 0; s < n; ++s) t |= ((L.get_info(s) >> 11) & 511) == pair;
+        if (!t && age + 1 < 3) {
+            L.cjn[(size_t)w * B + env] = L.cjn[(size_t)c * B + env];
             L.ckey[(size_t)w * B + env] = (uint16_t)(pair | ((age + 1) << 12));
             ++w;
         }
     }
     for (int s = 0; s < n; ++s) {
-        L.ckey[(size_t)w * B + env] = (uint16_t)((L.iget(s) >> 11) & 511);
-        L.cjn[(size_t)w * B + env] = L.rget(s, F_JN);
+        L.ckey[(size_t)w * B + env] = (uint16_t)((L.get_info(s) >> 11) & 511);
+        L.cjn[(size_t)w * B + env] = L.get_jn(s);
         ++w;
     }
     e.meta.set_ncache(w);
+    FUTBOL_STAMP(dtc == 2 ? 7 : 9);
 }
 
 // ---------------------------------------------------------------------------
@@ -415,16 +556,17 @@ template <int N, typename OT>
 __device__ __forceinline__ void write_obs(const Env<N>& e, OT* o)
 {
     using S = V1Shape<N>;
-    o[0] = (OT)((e.px[S::BALL] - 52.5) / 52.5);
-    o[1] = (OT)((e.py[S::BALL] - 34.0) / 34.0);
-    o[2] = (OT)((e.vx[S::BALL] - 0.0) / 25.0);
-    o[3] = (OT)((e.vy[S::BALL] - 0.0) / 25.0);
+    constexpr double r525 = 1.0 / 52.5, r555 = 1.0 / 55.5, r34 = 1.0 / 34.0, r25 = 1.0 / 25.0, r10 = 1.0 / 10.0;
+    o[0] = (OT)cdiv(e.px[S::BALL] - 52.5, 52.5, r525);
+    o[1] = (OT)cdiv(e.py[S::BALL] - 34.0, 34.0, r34);
+    o[2] = (OT)cdiv(e.vx[S::BALL] - 0.0, 25.0, r25);
+    o[3] = (OT)cdiv(e.vy[S::BALL] - 0.0, 25.0, r25);
     sfor<2 * N>([&](auto K) {
         constexpr int k = K;
-        o[4 + 4 * k + 0] = (OT)((e.px[k] - 52.5) / 55.5);
-        o[4 + 4 * k + 1] = (OT)((e.py[k] - 34.0) / 34.0);
-        o[4 + 4 * k + 2] = (OT)((e.vx[k] - 0.0) / 10.0);
-        o[4 + 4 * k + 3] = (OT)((e.vy[k] - 0.0) / 10.0);
+        o[4 + 4 * k + 0] = (OT)cdiv(e.px[k] - 52.5, 55.5, r555);
+        o[4 + 4 * k + 1] = (OT)cdiv(e.py[k] - 34.0, 34.0, r34);
+        o[4 + 4 * k + 2] = (OT)cdiv(e.vx[k] - 0.0, 10.0, r10);
+        o[4 + 4 * k + 3] = (OT)cdiv(e.vy[k] - 0.0, 10.0, r10);
     });
 }
 
@@ -460,9 +602,31 @@ __device__ __forceinline__ void store_env(const V1Ptrs& st, int env, int B, cons
     st.meta[env] = e.meta.w;
 }
 
+// the block's segment table in LDS (per-lane dynamic segment index in the collide loop)
+template <int N, int EPW>
+__device__ __forceinline__ void load_seg_table(const V1Params* __restrict__ P, Scratch<N, EPW>& sh)
+{
+    const int s = threadIdx.x;
+    if (s < kNSeg) {
+        SegLds g;
+        g.ax = P->sax[s];
+        g.ay = P->say[s];
+        g.sdx = P->sbx[s] - P->sax[s];
+        g.sdy = P->sby[s] - P->say[s];
+        g.L2 = P->L2[s];
+        g.rL2 = P->rL2[s];
+        sh.seg[s] = g;
+    }
+    __syncthreads();
+}
+
 // Futbol.reset (envs_v1/futbol_env.py:146-150): owner draw, formation, space.step(1e-4)
-template <int N>
-__device__ __forceinline__ void do_reset(const V1Params* __restrict__ P, const Lane<N>& L, Env<N>& e)
+template <int N, int EPW>
+__device__ __forceinline__ void do_reset(const V1Params* __restrict__ P, const Lane<N, EPW>& L, Env<N>& e
+#ifdef FUTBOL_STAMPS
+                                         , unsigned long long* st_stamps, unsigned long long& _stamp_prev
+#endif
+)
 {
     const uint32_t ev = e.meta.event();
     e.meta.set_event(ev + 1);
@@ -470,7 +634,11 @@ __device__ __forceinline__ void do_reset(const V1Params* __restrict__ P, const L
     e.meta.set_owner((uint32_t)rs.choice(2));
     e.meta.set_steps(0);
     position_to_initial<N>(P, e);
-    space_step<N>(P, L, e, 1);
+    space_step<N, EPW>(P, L, e, 1
+#ifdef FUTBOL_STAMPS
+                  , st_stamps, _stamp_prev
+#endif
+    );
 }
 
 // Team.get_pass_target_teammate (team.py:136-180) for player `me` of team `side`:
@@ -507,36 +675,43 @@ __device__ __forceinline__ void pass_target(const Env<N>& e, Stream& rs, int ar,
                 });
             }
         }
+        // select teammate t's position as tx = sum_q [q == t] * px[q] (exact: one term is
+        // 1 * px, the others +-0), so LLVM cannot turn it into a scratch-memory lookup table
         tx = 0.0;
         ty = 0.0;
         sfor<N>([&](auto Q) {
             constexpr int q = Q;
-            if (q == t) {
-                tx = e.px[base + q];
-                ty = e.py[base + q];
-            }
+            const double sel = q == t ? 1.0 : 0.0;
+            tx = __builtin_fma(sel, e.px[base + q], tx);
+            ty = __builtin_fma(sel, e.py[base + q], ty);
         });
     }
 }
 
 // ---------------------------------------------------------------------------
 // Futbol.step (envs_v1/futbol_env.py:427-483) + DummyVecEnv auto-reset
-template <int N, typename OT>
-__global__ void __launch_bounds__(64) v1_step_kernel(const V1Params* __restrict__ P, V1Ptrs st,
+template <int N, int EPW, typename OT>
+__global__ void __launch_bounds__(EPW) v1_step_kernel(const V1Params* __restrict__ P, V1Ptrs st,
                                                      const uint8_t* __restrict__ actions, OT* __restrict__ obs,
                                                      OT* __restrict__ reward, uint8_t* __restrict__ done_out,
                                                      OT* __restrict__ term_obs)
 {
     using S = V1Shape<N>;
     constexpr int BL = S::BALL;
-    __shared__ Scratch<N> sh;
-    const int env = blockIdx.x * 64 + threadIdx.x;
+    __shared__ Scratch<N, EPW> sh;
+    load_seg_table<N, EPW>(P, sh);
+    const int env = blockIdx.x * EPW + threadIdx.x;
     const int B = P->B;
     if (env >= B) return;
-    const Lane<N> L{&sh, st.spill, st.ckey, st.cjn, (int)threadIdx.x, env, B};
+    const Lane<N, EPW> L{&sh, st.spill, st.ckey, st.cjn, (int)threadIdx.x, env, B};
+#ifdef FUTBOL_STAMPS
+    unsigned long long* st_stamps = st.stamps;
+    unsigned long long _stamp_prev = __builtin_amdgcn_s_memtime();
+#endif
     Env<N> e;
     load_env<N>(st, env, B, e);
     const double W = P->W, H = P->H;
+    FUTBOL_STAMP(0);
 
     const uint32_t ev = e.meta.event();
     e.meta.set_event(ev + 1);
@@ -558,6 +733,7 @@ __global__ void __launch_bounds__(64) v1_step_kernel(const V1Params* __restrict_
         if constexpr (i & 1) key[N + (i >> 1)] = a; else arrow[N + (i >> 1)] = a;
     });
     if (bad) atomicAdd(st.invalid, (unsigned long long)bad);
+    FUTBOL_STAMP(1);
 
     // _ball_to_team_distance_arr(team_A), ball_init (:433-435)
     double d0[N];
@@ -632,7 +808,7 @@ __global__ void __launch_bounds__(64) v1_step_kernel(const V1Params* __restrict_
     if (!far_from_segments(e.px[BL], e.py[BL], 2.0, W, H)) {
         int w = -1;
         for (int s = 0; s < 6; ++s)
-            if (w < 0 && cs_hit(e.px[BL], e.py[BL], kBallR, P->sax[s], P->say[s], P->sbx[s], P->sby[s])) w = s;
+            if (w < 0 && cs_hit(P, s, e.px[BL], e.py[BL], kBallR)) w = s;
         if (w >= 0) {
             out = true;
             const double bx0 = e.px[BL], by0 = e.py[BL];
@@ -660,6 +836,7 @@ __global__ void __launch_bounds__(64) v1_step_kernel(const V1Params* __restrict_
         }
     }
     e.meta.set_owner(owner);
+    FUTBOL_STAMP(2);
 
     // Up to three cpSpaceSteps per call, through ONE inlined call site:
     //   phase 0: space.step(TIME_STEP) of this step            (:459)
@@ -667,6 +844,7 @@ __global__ void __launch_bounds__(64) v1_step_kernel(const V1Params* __restrict_
     //   phase 2: DummyVecEnv auto-reset -> reset(), step(1e-4) (:146-150)
     double r = 0.0, ret = 0.0;
     bool goal = false, done = false;
+#pragma unroll 1
     for (int ph = 0; ph < 3; ++ph) {
         if (ph == 1 && !goal) continue;
         if (ph == 2 && !(done && P->auto_reset)) continue;
@@ -683,7 +861,12 @@ __global__ void __launch_bounds__(64) v1_step_kernel(const V1Params* __restrict_
             e.meta.set_steps(0);
             position_to_initial<N>(P, e);
         }
-        space_step<N>(P, L, e, ph == 0 ? 2 : 1);
+        FUTBOL_STAMP(ph == 0 ? 3 : 9);
+        space_step<N, EPW>(P, L, e, ph == 0 ? 2 : 1
+#ifdef FUTBOL_STAMPS
+                      , st_stamps, _stamp_prev
+#endif
+        );
         if (ph == 0) {
             if (!out) {  // get_team_reward + get_ball_reward (:493-515)
                 double mx = 0.0;
@@ -706,8 +889,7 @@ __global__ void __launch_bounds__(64) v1_step_kernel(const V1Params* __restrict_
             }
             // ball_contact_goal (:291-296); a goal restarts from formation, the episode goes on
             if (!far_from_segments(e.px[BL], e.py[BL], 2.0, W, H)) {
-                for (int s = 6; s < 12; ++s)
-                    goal = goal || cs_hit(e.px[BL], e.py[BL], kBallR, P->sax[s], P->say[s], P->sbx[s], P->sby[s]);
+                for (int s = 6; s < 12; ++s) goal = goal || cs_hit(P, s, e.px[BL], e.py[BL], kBallR);
             }
             if (goal) r = r + (e.px[BL] > W - 2 ? 1000.0 : -1000.0);
             // current_time += 0.1; done = current_time > total_time
@@ -726,28 +908,31 @@ __global__ void __launch_bounds__(64) v1_step_kernel(const V1Params* __restrict_
         } else if (ph == 1) {
             e.meta.set_owner((uint32_t)rs.choice(2));  // random.choice(["left","right"]) (:475)
         }
+        FUTBOL_STAMP(ph == 0 ? 8 : 9);
     }
     write_obs<N, OT>(e, obs + (size_t)env * (4 * S::Nb));
     st.ep_ret[env] = ret;
     reward[env] = (OT)r;
     done_out[env] = done ? 1 : 0;
     store_env<N>(st, env, B, e);
+    FUTBOL_STAMP(10);
     if (env == 0) *st.act_step += 1;  // stream-ordered after this step's fill_actions
 }
 
 // futbol_create (init=1: Futbol.__init__, which ends in reset()) / futbol_reset (masked)
-template <int N, typename OT>
-__global__ void __launch_bounds__(64) v1_reset_kernel(const V1Params* __restrict__ P, V1Ptrs st,
+template <int N, int EPW, typename OT>
+__global__ void __launch_bounds__(EPW) v1_reset_kernel(const V1Params* __restrict__ P, V1Ptrs st,
                                                       const uint8_t* __restrict__ mask, OT* __restrict__ obs,
                                                       int init)
 {
     using S = V1Shape<N>;
-    __shared__ Scratch<N> sh;
-    const int env = blockIdx.x * 64 + threadIdx.x;
+    __shared__ Scratch<N, EPW> sh;
+    load_seg_table<N, EPW>(P, sh);
+    const int env = blockIdx.x * EPW + threadIdx.x;
     const int B = P->B;
     if (env >= B) return;
     if (mask && !mask[env]) return;
-    const Lane<N> L{&sh, st.spill, st.ckey, st.cjn, (int)threadIdx.x, env, B};
+    const Lane<N, EPW> L{&sh, st.spill, st.ckey, st.cjn, (int)threadIdx.x, env, B};
     Env<N> e;
     if (init) {
         sfor<S::Nb>([&](auto K) {
@@ -763,7 +948,15 @@ __global__ void __launch_bounds__(64) v1_reset_kernel(const V1Params* __restrict
         load_env<N>(st, env, B, e);
     }
     st.ep_ret[env] = 0.0;
-    do_reset<N>(P, L, e);
+#ifdef FUTBOL_STAMPS
+    unsigned long long* st_stamps = nullptr;
+    unsigned long long _stamp_prev = 0;
+#endif
+    do_reset<N, EPW>(P, L, e
+#ifdef FUTBOL_STAMPS
+                , st_stamps, _stamp_prev
+#endif
+    );
     if (obs) write_obs<N, OT>(e, obs + (size_t)env * (4 * S::Nb));
     store_env<N>(st, env, B, e);
 }

@@ -1,0 +1,31 @@
+// futbol_v1_n10_e32.hip -- instantiation of the envs_v1 kernels for N = 10 players per team,
+// 32 envs per one-wave block (one translation unit per variant: they compile in parallel).
+#include "futbol_v1_impl.hpp"
+
+namespace futbol {
+
+int launch_v1_n10_e32(const V1Params* P, int B, const V1Ptrs& st, int out64, int what, const uint8_t* actions,
+                      const uint8_t* mask, void* obs, void* reward, uint8_t* done, void* term, int init,
+                      hipStream_t stream)
+{
+    constexpr int N = 10, E = 32;
+    const dim3 grid((B + E - 1) / E), block(E);
+    if (what == 0) {
+        if (out64)
+            hipLaunchKernelGGL((v1_step_kernel<N, E, double>), grid, block, 0, stream, P, st, actions, (double*)obs,
+                               (double*)reward, done, (double*)term);
+        else
+            hipLaunchKernelGGL((v1_step_kernel<N, E, float>), grid, block, 0, stream, P, st, actions, (float*)obs,
+                               (float*)reward, done, (float*)term);
+    } else {
+        if (out64)
+            hipLaunchKernelGGL((v1_reset_kernel<N, E, double>), grid, block, 0, stream, P, st, mask, (double*)obs,
+                               init);
+        else
+            hipLaunchKernelGGL((v1_reset_kernel<N, E, float>), grid, block, 0, stream, P, st, mask, (float*)obs,
+                               init);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace futbol

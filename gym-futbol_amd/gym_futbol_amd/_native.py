@@ -9,6 +9,9 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libfutbol_amd.so")
+# diagnostic builds (bench.py --stamps) are selected by name, always from this directory
+if os.environ.get("FUTBOL_LIB_VARIANT"):
+    LIB_PATH = os.path.join(HERE, "libfutbol_amd_%s.so" % os.environ["FUTBOL_LIB_VARIANT"])
 
 ENV_V0, ENV_V1 = 0, 1
 F32, F64 = 0, 1
@@ -50,6 +53,7 @@ SIGNATURES = [
     ("futbol_get_state", C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]),
     ("futbol_set_state", C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]),
     ("futbol_episode_limit", C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
+    ("futbol_debug_stamps", C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32]),
 ]
 
 _lib = None

@@ -122,6 +122,10 @@ int futbol_set_state(FutbolCtx* ctx, const void* src, int32_t src_is_host, void*
    (the reference accumulates current_time += 0.1 in fp64). */
 int futbol_episode_limit(const FutbolCtx* ctx, int32_t* steps);
 
+/* Diagnostic builds only (compiled with -DFUTBOL_STAMPS; FUTBOL_EUNSUPPORTED otherwise):
+   per-64-env-block sums of s_memtime cycles spent in each step phase, [blocks][16] u64. */
+int futbol_debug_stamps(FutbolCtx* ctx, uint64_t* host_out, int64_t n, int32_t clear);
+
 #ifdef __cplusplus
 }
 #endif
