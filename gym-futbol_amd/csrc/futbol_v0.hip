@@ -126,7 +126,7 @@ __device__ __forceinline__ void set_vector_observation(const Ctx& c, Env& e, boo
             (void)c.rs->randint(0, 9);
             const double ang = (nd / 180) * 3.141592653589793;
             double ss, sc;
-            pm_sincos(ang, &ss, &sc);
+            cr_sincos(ang, &ss, &sc);
             const double tc = (cs * sc) - (sn * ss), ts = (sn * sc) + (cs * ss);
             ball[2] = tc * mag;
             ball[3] = ts * mag;

@@ -20,7 +20,9 @@
  *   randint(a,b) = a + choice(b-a+1)
  *   uniform(a,b) = a + (b-a)*U          (CPython random.uniform form)
  *   normal(mu,sigma) = mu + sigma*Z,  Z = sqrt(-2 ln(1-U1)) * cos(2 pi U2)
- *                      U1 from (x0,x1), U2 from (x2,x3)
+ *                      U1 from (x0,x1), U2 from (x2,x3); ln and cos are the
+ *                      specified +,-,*,/-only orc_pm_log / orc_pm_sincos
+ *                      (oracle_math.h), so Z is the same double everywhere
  */
 #ifndef ORACLE_RNG_H
 #define ORACLE_RNG_H
@@ -97,7 +99,7 @@ static inline double oracle_normal(OracleRng *g, double mu, double sigma)
     oracle_rng_block(g, x);
     double u1 = oracle_u53(x[0], x[1]);
     double u2 = oracle_u53(x[2], x[3]);
-    double z = sqrt(-2.0 * ORC_LOG(1.0 - u1)) * ORC_COS(6.283185307179586 * u2);
+    double z = orc_tape_z(u1, u2);
     return mu + sigma * z;
 }
 
