@@ -66,6 +66,23 @@ def cpu_baseline(kind, n, budget_s=12.0, B=65536):
                       % ("envs_v1 2v2" if kind == "v1" else "v0 hard-coded-opponent", B, steps, dt)}
 
 
+def pmc_traffic(kind, n, B):
+    """HBM bytes per step-kernel launch from the committed rocprofv3 --pmc pass of this
+    same configuration (scripts/gpu_profile.sh -> scripts/pmc_traffic.py ->
+    profiles/<round>/traffic.json), or (None, None) when no matching entry exists."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic.json")), reverse=True):
+        try:
+            with open(path) as f:
+                entries = json.load(f)
+        except (OSError, ValueError):
+            continue
+        for e in entries:
+            if e.get("kind") == kind and e.get("players", n) == n and e.get("envs") == B:
+                return e["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+    return None, None
+
+
 STAMP_SLOTS = ["load state", "actions + opponent RNG", "process_action + out-of-bounds", "phase glue",
                "integrate p + collide", "cache lookups + integrate v", "warm start + 10 solver iterations",
                "arbiter cache update", "reward / goal / time", "goal reset + auto-reset phases", "obs + store"]
@@ -105,29 +122,22 @@ def main():
     ap.add_argument("--kind", default="v1", choices=["v1", "v0"])
     ap.add_argument("--graph", type=int, default=1, help="replay the timed steps from a hipGraph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--profile-steps", type=int, default=200, help="steps timed per-kernel with HIP events")
+    ap.add_argument("--profile-steps", type=int, default=600,
+                    help="steps timed per-kernel with HIP events (a multiple of the episode length)")
     ap.add_argument("--stamps", action="store_true",
                     help="diagnostic: load the FUTBOL_STAMPS build and print the per-phase cycle breakdown")
     args = ap.parse_args()
     if args.stamps:
         os.environ["FUTBOL_LIB_VARIANT"] = "stamps"
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
-
     from gym_futbol_amd import FutbolVecEnv
+    from gym_futbol_amd import distributed as D
+    R = D.init(use_gpu=True)          # one process per GPU; RCCL when world > 1
+    rank, world, dev = R.rank, R.world, R.device
     B = args.envs
     n = args.players
     kw = {"number_of_player": n} if args.kind == "v1" else {"random_opp": False}
-    venv = FutbolVecEnv(args.kind, B, device=dev, seed=0, env_id_base=rank * B, dtype=torch.float32, **kw)
+    venv = FutbolVecEnv(args.kind, B, device=dev, seed=0, env_id_base=R.shard(B), dtype=torch.float32, **kw)
     venv.reset()
     act = venv._act
     stream = torch.cuda.current_stream(dev)
@@ -141,16 +151,14 @@ def main():
         one_step()
     torch.cuda.synchronize(dev)
 
-    # per-kernel timing of the dominant kernel (the env step) with HIP events on its stream
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.profile_steps)]
-    for e0, e1 in ev:
-        venv.random_actions(ALL, seed=1234, out=act)
-        e0.record(stream)
-        venv.step_raw(act)
-        e1.record(stream)
-    torch.cuda.synchronize(dev)
-    kernel_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ev]))
+    # per-kernel timing of the dominant kernel (the env step): HIP events stamped by the
+    # dispatch itself (hipExtLaunchKernelGGL on the launch stream), over whole episodes
+    # (all envs start together, so the step cost varies with the episode phase)
+    venv.kernel_timing(True)
+    for _ in range(args.profile_steps):
+        one_step()
+    tot_ms, cnt = venv.kernel_timing(False)
+    kernel_ms = tot_ms / max(cnt, 1)
 
     if args.stamps:
         return stamps_report(venv, one_step, args)
@@ -170,8 +178,7 @@ def main():
 
     stats_buf = torch.zeros(3, dtype=torch.float64, device=dev)
     venv.episode_stats(clear=True)
-    if dist is not None:
-        dist.barrier()
+    D.barrier(dev)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     done_steps = 0
@@ -184,28 +191,20 @@ def main():
                 one_step()
         prev = done_steps
         done_steps += chunk
-        if dist is not None and done_steps // 300 != prev // 300:
+        if R.distributed and done_steps // 300 != prev // 300:
             stats_buf.copy_(venv.episode_stats(clear=False))
-            dist.all_reduce(stats_buf)  # RCCL over xGMI: [sum return, episodes, env-steps]
+            D.reduce_episode_stats(stats_buf)  # RCCL over xGMI: [sum return, episodes, env-steps]
     torch.cuda.synchronize(dev)
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    stats = venv.episode_stats(clear=False).cpu().numpy()
-    if dist is not None:
-        st = torch.as_tensor(stats, device=dev)
-        dist.all_reduce(st)
-        stats = st.cpu().numpy()
+    D.barrier(dev)
+    elapsed = D.max_over_ranks(time.perf_counter() - t0, dev)
+    stats = D.reduce_episode_stats(venv.episode_stats(clear=False).clone()).cpu().numpy()
 
     total_env_steps = B * args.steps * world
     value = total_env_steps / elapsed
     out_bytes = 4
     per_env = algo_bytes_per_env_step(args.kind, n, out_bytes)
     achieved = per_env * B / (kernel_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(args.kind, n, B)
     line = {
         "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
@@ -216,9 +215,10 @@ def main():
                    "envs_per_gpu": B, "global_envs": B * world, "parallelism": "dp%d" % world,
                    "obs_dtype": "f32", "hip_graph": bool(graph is not None)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "v1_step_kernel<%d,float>" % n if args.kind == "v1" else "v0_step_kernel<float>",
-                     "kernel_ms": kernel_ms, "algo_bytes_per_env_step": per_env},
+                     "kernel_ms": kernel_ms, "algo_bytes_per_launch": per_env * B,
+                     "algo_bytes_per_env_step": per_env, "traffic_source": traffic_src},
         "episodes": {"finished": float(stats[1]),
                      "mean_return": float(stats[0] / stats[1]) if stats[1] else None},
     }
@@ -227,8 +227,7 @@ def main():
     if rank == 0:
         print(json.dumps(line), flush=True)
     venv.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    D.shutdown()
 
 
 if __name__ == "__main__":

@@ -46,6 +46,10 @@ struct FutbolCtx {
     V0Ptrs v0{};
     double steps_since_clear = 0.0;
     unsigned long long* d_stamps = nullptr;  // diagnostic builds (FUTBOL_STAMPS) only
+    // futbol_kernel_timing: one (start, stop) event pair per timed step launch
+    std::vector<hipEvent_t> t_ev;
+    int64_t t_count = 0;
+    bool timing = false;
     std::string err;
 };
 
@@ -407,6 +411,8 @@ extern "C" int futbol_destroy(FutbolCtx* ctx)
     if (ctx->d_params) hipFree(ctx->d_params);
     if (ctx->d_invalid) hipFree(ctx->d_invalid);
     if (ctx->d_stamps) hipFree(ctx->d_stamps);
+    for (auto e : ctx->t_ev)
+        if (e) hipEventDestroy(e);
     delete ctx;
     return FUTBOL_OK;
 }
@@ -432,11 +438,49 @@ extern "C" int futbol_episode_limit(const FutbolCtx* ctx, int32_t* steps)
     return FUTBOL_OK;
 }
 
+namespace futbol {
+thread_local LaunchEvents g_launch_events;
+}
+
+static constexpr int64_t kTimingCap = 8192;
+
+extern "C" int futbol_kernel_timing(FutbolCtx* ctx, int32_t mode, double* total_ms, int64_t* count)
+{
+    if (!ctx || (mode != 0 && mode != 1)) return FUTBOL_EINVAL;
+    FB_CHECK_HIP(ctx, hipSetDevice(ctx->device));
+    if (mode == 1) {
+        if (ctx->t_ev.empty()) {
+            ctx->t_ev.resize(2 * kTimingCap, nullptr);
+            for (auto& e : ctx->t_ev) FB_CHECK_HIP(ctx, hipEventCreate(&e));
+        }
+        ctx->t_count = 0;
+        ctx->timing = true;
+        return FUTBOL_OK;
+    }
+    ctx->timing = false;
+    double tot = 0.0;
+    for (int64_t i = 0; i < ctx->t_count; ++i) {
+        float ms = 0.f;
+        FB_CHECK_HIP(ctx, hipEventSynchronize(ctx->t_ev[2 * i + 1]));
+        FB_CHECK_HIP(ctx, hipEventElapsedTime(&ms, ctx->t_ev[2 * i], ctx->t_ev[2 * i + 1]));
+        tot += ms;
+    }
+    if (total_ms) *total_ms = tot;
+    if (count) *count = ctx->t_count;
+    return FUTBOL_OK;
+}
+
 static int launch(FutbolCtx* ctx, int what, const uint8_t* actions, const uint8_t* mask, void* obs, void* reward,
                   uint8_t* done, void* term, void* stream)
 {
     FB_CHECK_HIP(ctx, hipSetDevice(ctx->device));
     const int out64 = ctx->cfg.out_dtype == FUTBOL_F64;
+    const bool timed = what == 0 && ctx->timing && ctx->t_count < kTimingCap;
+    if (timed) {
+        g_launch_events.start = ctx->t_ev[2 * ctx->t_count];
+        g_launch_events.stop = ctx->t_ev[2 * ctx->t_count + 1];
+        ctx->t_count++;
+    }
     int rc;
     if (ctx->cfg.env_kind == FUTBOL_ENV_V1)
         rc = launch_v1(ctx->N, ctx->epw, (const V1Params*)ctx->d_params, ctx->B, ctx->v1, out64, what, actions,
@@ -444,6 +488,7 @@ static int launch(FutbolCtx* ctx, int what, const uint8_t* actions, const uint8_
     else
         rc = launch_v0((const V0Params*)ctx->d_params, ctx->B, ctx->v0, out64, what, actions, mask, obs, reward,
                        done, term, 0, (hipStream_t)stream);
+    g_launch_events = LaunchEvents{};
     if (rc) {
         hipError_t e = hipGetLastError();
         return fail(ctx, FUTBOL_EHIP, std::string("kernel launch failed: ") + hipGetErrorString(e));

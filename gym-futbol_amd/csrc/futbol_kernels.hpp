@@ -2,6 +2,7 @@
 // and the env kernels (futbol_v1.hip, futbol_v0.hip).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stddef.h>
 #include <stdint.h>
 #include "futbol_state.hpp"
@@ -49,6 +50,25 @@ struct V0Params {
     int K_done;                                   // steps until time >= game_time
     int auto_reset;
 };
+
+// Kernel timing (futbol_kernel_timing): when `start` is set, the next env-step launch
+// goes through hipExtLaunchKernelGGL, whose events are stamped by the dispatch itself
+// (kernel begin / end, no marker packets around it).  Set by the C ABI, host thread-local.
+struct LaunchEvents {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+extern thread_local LaunchEvents g_launch_events;
+
+template <typename... KArgs, typename... Args>
+inline void launch_kernel(void (*k)(KArgs...), dim3 grid, dim3 block, hipStream_t stream, Args... args)
+{
+    static_assert(sizeof...(KArgs) == sizeof...(Args), "kernel argument count");
+    if (g_launch_events.start)
+        hipExtLaunchKernelGGL(k, grid, block, 0, stream, g_launch_events.start, g_launch_events.stop, 0,
+                              static_cast<KArgs>(args)...);
+    else
+        hipLaunchKernelGGL(k, grid, block, 0, stream, static_cast<KArgs>(args)...);
+}
 
 // P: device pointer to the context's V1Params (wave-uniform scalar loads)
 int launch_v1(int N, int epw, const V1Params* P, int B, const V1Ptrs& st, int out64, int what,

@@ -531,10 +531,10 @@ int launch_v0(const V0Params* P, int B, const V0Ptrs& st, int out64, int what, c
     const dim3 grid((B + 63) / 64), block(64);
     if (what == 0) {
         if (out64)
-            hipLaunchKernelGGL((v0_step_kernel<double>), grid, block, 0, stream, P, st, actions, (double*)obs,
+            launch_kernel(v0_step_kernel<double>, grid, block, stream, P, st, actions, (double*)obs,
                                (double*)reward, done, (double*)term);
         else
-            hipLaunchKernelGGL((v0_step_kernel<float>), grid, block, 0, stream, P, st, actions, (float*)obs,
+            launch_kernel(v0_step_kernel<float>, grid, block, stream, P, st, actions, (float*)obs,
                                (float*)reward, done, (float*)term);
     } else {
         if (out64)

@@ -12,10 +12,10 @@ int launch_v1_n10_e32(const V1Params* P, int B, const V1Ptrs& st, int out64, int
     const dim3 grid((B + E - 1) / E), block(E);
     if (what == 0) {
         if (out64)
-            hipLaunchKernelGGL((v1_step_kernel<N, E, double>), grid, block, 0, stream, P, st, actions, (double*)obs,
+            launch_kernel(v1_step_kernel<N, E, double>, grid, block, stream, P, st, actions, (double*)obs,
                                (double*)reward, done, (double*)term);
         else
-            hipLaunchKernelGGL((v1_step_kernel<N, E, float>), grid, block, 0, stream, P, st, actions, (float*)obs,
+            launch_kernel(v1_step_kernel<N, E, float>, grid, block, stream, P, st, actions, (float*)obs,
                                (float*)reward, done, (float*)term);
     } else {
         if (out64)

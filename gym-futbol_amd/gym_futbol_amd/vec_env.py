@@ -147,6 +147,15 @@ class FutbolVecEnv:
                       self.ctx.h)
         return v.value
 
+    def kernel_timing(self, start):
+        """start=True: time the following step launches with dispatch-stamped HIP events;
+        start=False: stop and return (total kernel ms, number of timed launches)."""
+        tot, cnt = C.c_double(), C.c_int64()
+        with torch.cuda.device(self.device):
+            nat.check(nat.load().futbol_kernel_timing(self.ctx.h, 1 if start else 0, C.byref(tot), C.byref(cnt)),
+                      self.ctx.h)
+        return tot.value, cnt.value
+
     # ------------------------------------------------------------ state I/O
     def get_state(self):
         """Host copy of the SoA state: {field: numpy array} (see csrc/futbol_state.hpp)."""

@@ -126,6 +126,13 @@ int futbol_episode_limit(const FutbolCtx* ctx, int32_t* steps);
    per-64-env-block sums of s_memtime cycles spent in each step phase, [blocks][16] u64. */
 int futbol_debug_stamps(FutbolCtx* ctx, uint64_t* host_out, int64_t n, int32_t clear);
 
+/* Kernel timing (measurement, not part of the reference interface).  mode 1: start
+ * timing the following futbol_step launches (up to 8192) with HIP events stamped by
+ * the dispatch itself (hipExtLaunchKernelGGL: kernel begin/end on the launch stream);
+ * mode 0: stop, wait for the last timed launch and return the summed kernel time and
+ * the number of timed launches.  Not usable inside hipGraph capture. */
+int futbol_kernel_timing(FutbolCtx* ctx, int32_t mode, double* total_ms, int64_t* count);
+
 #ifdef __cplusplus
 }
 #endif

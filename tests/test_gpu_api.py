@@ -1,0 +1,242 @@
+"""The drop-in surface on the GPU: registered ids through make(), the single-env
+facades (envs_v1.Futbol, envs.FutbolEnv) against the oracle, masked reset,
+state save/restore, out-of-range actions, device episode statistics, the
+synthetic-action stream against the Python tape, and the stable-baselines
+adapter.  Bit-exact comparisons are against oracle/liboracle_portable.so."""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+import gym_futbol_amd as gf
+from helpers import O
+from rng_tape import synthetic_action
+
+pytestmark = pytest.mark.gpu
+
+
+def _rollout_dones(venv, T, nvals):
+    rng = np.random.default_rng(0)
+    dones = []
+    for t in range(T):
+        a = torch.as_tensor(rng.integers(0, nvals, (venv.num_envs, venv.action_dim)), dtype=torch.uint8)
+        _, _, d, _ = venv.step(a)
+        dones.append(d.cpu().numpy().copy())
+    return np.stack(dones, 1)
+
+
+@pytest.mark.parametrize("env_id,B,T,period,nvals", [("Futbol2v2-v1", 256, 620, 300, 5),
+                                                     ("Futbol5v5-v1", 64, 310, 300, 5),
+                                                     ("Futbol-v1", 32, 305, 300, 5),
+                                                     ("Futbol-v0", 128, 820, 401, 16)])
+def test_make_and_episode_lengths(env_id, B, T, period, nvals):
+    """K1/K7: every episode lasts exactly 300 (v1, total_time 30 / dt 0.1) or 401 (v0) steps."""
+    venv = gf.make(env_id, num_envs=B, seed=11)
+    assert venv.episode_steps == period
+    venv.reset()
+    d = _rollout_dones(venv, T, nvals)
+    expect = np.zeros(T, bool)
+    expect[period - 1::period] = True
+    assert (d == expect[None, :]).all()
+    venv.close()
+
+
+def test_futbol_facade_matches_oracle():
+    """envs_v1.Futbol API (B = 1, fp64, no auto-reset), default number_of_player=5."""
+    f = gf.Futbol(seed=3, env_id=7)
+    ora = O.V1Vec(1, N=5, seed=3, env_id_base=7, portable=True)
+    assert f.observation_space.shape == (44,) and f.action_space.nvec.tolist() == [5, 5] * 5
+    assert np.array_equal(f.reset(), ora.reset()[0])
+    rng = np.random.default_rng(1)
+    for t in range(300):
+        a = rng.integers(0, 5, 10)
+        o, r, d, info = f.step(a)
+        o2, r2, d2, term2 = ora.step(a[None])
+        assert info == {} and isinstance(r, float) and isinstance(d, bool)
+        exp = term2[0] if d2[0] else o2[0]     # the oracle auto-resets; the facade does not
+        assert d == bool(d2[0]) and r == r2[0] and np.array_equal(o, exp), t
+    assert d and abs(f.current_time - 30.0) < 1e-9
+    assert f.ball_owner_side in ("left", "right")
+    o, r, d, _ = f.step(rng.integers(0, 5, 10))   # like the reference: done stays True past the end
+    assert d
+    with pytest.raises(ValueError):
+        f.step([5] + [0] * 9)
+    with pytest.raises(ValueError):
+        f.step([0] * 4)
+    f.close()
+
+
+@pytest.mark.parametrize("random_opp", [False, True])
+def test_futbolenv_facade_matches_oracle(random_opp):
+    """envs.FutbolEnv API (B = 1, fp64, no auto-reset)."""
+    f = gf.FutbolEnv(random_opp=random_opp, seed=5, env_id=2)
+    ora = O.V0Vec(1, seed=5, env_id_base=2, random_opp=random_opp, portable=True)
+    assert np.array_equal(f.reset(), ora.reset()[0])
+    rng = np.random.default_rng(4)
+    for t in range(401):
+        a = int(rng.integers(0, 16))
+        o, r, d, _ = f.step(a)
+        o2, r2, d2, term2 = ora.step(np.array([a]))
+        exp = term2[0] if d2[0] else o2[0]
+        assert d == bool(d2[0]) and r == r2[0] and np.array_equal(o, exp), t
+    assert d and f.time > 40
+    assert 0 <= f.ball_owner <= 4 and 0 <= f.last_ball_owner <= 4
+    assert f.ai_score >= 0 and f.opp_score >= 0
+    with pytest.raises(ValueError):
+        f.step(16)
+    f.close()
+    g = gf.FutbolEnv(action_as_int=False, seed=1)
+    assert [s.n for s in g.action_space.spaces] == [4, 4]
+    g.reset()
+    o, r, d, _ = g.step((2, 3))
+    assert o.shape == (6, 5)
+    with pytest.raises(ValueError):
+        g.step((4, 0))
+    g.close()
+
+
+def test_masked_reset_v1():
+    B, n = 96, 2
+    venv = gf.FutbolVecEnv("v1", B, seed=21, dtype=torch.float64, number_of_player=n)
+    ora = O.V1Vec(B, N=n, seed=21, portable=True)
+    venv.reset()
+    ora.reset()
+    rng = np.random.default_rng(3)
+    for t in range(40):
+        a = rng.integers(0, 5, (B, 2 * n))
+        o, _, _, _ = venv.step(a)
+        o2, _, _, _ = ora.step(a)
+    before = o.cpu().numpy().copy()
+    mask = np.zeros(B, np.uint8)
+    mask[::3] = 1
+    after = venv.reset(mask).cpu().numpy()
+    for i in np.nonzero(mask)[0]:
+        row = np.zeros(ora.obs_dim)
+        ora.L.orc_v1_reset(C.byref(ora.envs[i]), row.ctypes.data)
+        assert np.array_equal(after[i], row)
+    keep = mask == 0
+    assert np.array_equal(after[keep], before[keep])
+    for t in range(30):
+        a = rng.integers(0, 5, (B, 2 * n))
+        o, r, d, _ = venv.step(a)
+        o2, r2, d2, _ = ora.step(a)
+        assert np.array_equal(o.cpu().numpy(), o2) and np.array_equal(r.cpu().numpy(), r2)
+    venv.close()
+
+
+@pytest.mark.parametrize("kind,kw,nvals,adim", [("v1", {"number_of_player": 5}, 5, 10), ("v0", {}, 16, 1)])
+def test_state_save_restore(kind, kw, nvals, adim):
+    B = 64
+    a_env = gf.FutbolVecEnv(kind, B, seed=8, dtype=torch.float64, **kw)
+    b_env = gf.FutbolVecEnv(kind, B, seed=8, dtype=torch.float64, **kw)
+    a_env.reset()
+    b_env.reset()
+    rng = np.random.default_rng(9)
+    for t in range(57):
+        a_env.step(rng.integers(0, nvals, (B, adim)))
+    st = a_env.get_state()
+    b_env.set_state(st)
+    st2 = b_env.get_state()
+    for k in st:
+        assert np.array_equal(st[k], st2[k]), k
+    for t in range(260):
+        a = rng.integers(0, nvals, (B, adim))
+        oa, ra, da, _ = a_env.step(a)
+        ob, rb, db, _ = b_env.step(a)
+        assert np.array_equal(oa.cpu().numpy(), ob.cpu().numpy()), t
+        assert np.array_equal(ra.cpu().numpy(), rb.cpu().numpy()) and np.array_equal(da.cpu().numpy(),
+                                                                                   db.cpu().numpy())
+    with pytest.raises(ValueError):
+        b_env.set_state({**st, "px" if kind == "v1" else "row": np.zeros(3)})
+    a_env.close()
+    b_env.close()
+
+
+@pytest.mark.parametrize("kind,kw,adim,hi", [("v1", {"number_of_player": 2}, 4, 4), ("v0", {}, 1, 15)])
+def test_out_of_range_actions_are_clamped_and_counted(kind, kw, adim, hi):
+    B = 128
+    x = gf.FutbolVecEnv(kind, B, seed=2, dtype=torch.float64, **kw)
+    y = gf.FutbolVecEnv(kind, B, seed=2, dtype=torch.float64, **kw)
+    x.reset()
+    y.reset()
+    rng = np.random.default_rng(6)
+    nbad = 0
+    for t in range(30):
+        a = rng.integers(0, hi + 1, (B, adim))
+        bad = a.copy()
+        sel = rng.random(a.shape) < 0.05
+        bad[sel] = hi + 1 + rng.integers(0, 100, sel.sum())
+        nbad += int(sel.sum())
+        ox = x.step(bad)[0].cpu().numpy()
+        oy = y.step(np.where(sel, hi, a))[0].cpu().numpy()
+        assert np.array_equal(ox, oy)
+    assert x.invalid_actions() == nbad and y.invalid_actions() == 0
+    with pytest.raises(ValueError):
+        x.step(-np.ones((B, adim)))
+    x.close()
+    y.close()
+
+
+def test_episode_stats_on_device():
+    B, n, T = 200, 2, 650
+    venv = gf.FutbolVecEnv("v1", B, seed=31, dtype=torch.float64, number_of_player=n)
+    venv.reset()
+    venv.episode_stats(clear=True)
+    ret = np.zeros(B)
+    fin_ret, fin_cnt = np.zeros(B), 0
+    for t in range(T):
+        _, r, d, _ = venv.step(venv.random_actions(t, seed=5))
+        ret += r.cpu().numpy()
+        dn = d.cpu().numpy()
+        fin_ret[dn] += ret[dn]
+        fin_cnt += int(dn.sum())
+        ret[dn] = 0
+    s = venv.episode_stats().cpu().numpy()
+    assert s[1] == fin_cnt == 2 * B
+    assert np.isclose(s[0], fin_ret.sum(), rtol=1e-12, atol=1e-9)
+    assert s[2] == B * T
+    s = venv.episode_stats(clear=True).cpu().numpy()
+    s = venv.episode_stats().cpu().numpy()
+    assert s[0] == 0 and s[1] == 0
+    venv.close()
+
+
+@pytest.mark.parametrize("kind,kw,nvals", [("v1", {"number_of_player": 3}, 5), ("v0", {}, 16)])
+def test_random_actions_follow_the_tape(kind, kw, nvals):
+    B, base = 40, 1000
+    venv = gf.FutbolVecEnv(kind, B, seed=1, env_id_base=base, **kw)
+    for step in (0, 7, 123456):
+        a = venv.random_actions(step, seed=99).cpu().numpy()
+        exp = np.array([[synthetic_action(99, base + i, step, j, nvals) for j in range(venv.action_dim)]
+                        for i in range(B)])
+        assert np.array_equal(a, exp)
+    venv.close()
+
+
+def test_sb3_adapter():
+    venv = gf.make("Futbol2v2-v1", num_envs=16, seed=4)
+    sb = venv.as_sb3()
+    o = sb.reset()
+    assert o.shape == (16, 20) and o.dtype == np.float32
+    rng = np.random.default_rng(0)
+    for t in range(300):
+        o, r, d, infos = sb.step(rng.integers(0, 5, (16, 4)))
+    assert o.dtype == np.float32 and r.dtype == np.float32 and d.all()
+    for i in range(16):
+        assert infos[i]["terminal_observation"].shape == (20,)
+        assert infos[i]["episode"]["l"] == 300
+    assert sb.get_attr("number_of_player") == [2] * 16
+    sb.close()
+
+
+def test_kernel_timing_counts_step_launches():
+    venv = gf.make("Futbol2v2-v1", num_envs=4096, seed=0)
+    venv.reset()
+    venv.kernel_timing(True)
+    for t in range(25):
+        venv.step(venv.random_actions(t))
+    venv.reset()                                  # reset launches are not timed
+    tot, cnt = venv.kernel_timing(False)
+    assert cnt == 25 and 0 < tot / cnt < 50.0    # ms per launch
+    venv.close()
