@@ -151,18 +151,41 @@ def main():
         one_step()
     torch.cuda.synchronize(dev)
 
-    # per-kernel timing of the dominant kernel (the env step): HIP events stamped by the
-    # dispatch itself (hipExtLaunchKernelGGL on the launch stream), over whole episodes
-    # (all envs start together, so the step cost varies with the episode phase)
+    # per-kernel timing of the dominant kernel (the env step), two ways, over whole episodes
+    # (all envs start together, so the per-step cost varies with the episode phase):
+    #  (1) HIP events around a hipGraph of `profile_steps` back-to-back step launches with
+    #      pre-generated actions (the way the kernel runs in the timed region) -> kernel_ms
+    #  (2) events stamped by each dispatch (hipExtLaunchKernelGGL)           -> kernel_ms_dispatch
+    acts = torch.empty((args.profile_steps,) + tuple(act.shape), dtype=torch.uint8, device=dev)
+    for t in range(args.profile_steps):
+        venv.random_actions(10**6 + t, seed=1234, out=acts[t])
+    kg = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(stream)
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(kg, stream=s):
+            for t in range(args.profile_steps):
+                venv.step_raw(acts[t])
+    stream.wait_stream(s)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    kg.replay()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    kernel_ms = e0.elapsed_time(e1) / args.profile_steps
+    del kg, acts
     venv.kernel_timing(True)
     for _ in range(args.profile_steps):
         one_step()
     tot_ms, cnt = venv.kernel_timing(False)
-    kernel_ms = tot_ms / max(cnt, 1)
+    kernel_ms_dispatch = tot_ms / max(cnt, 1)
 
     if args.stamps:
         return stamps_report(venv, one_step, args)
 
+    # timed loop: hipGraph of G steps (fill_actions + step each).  Forking the fill onto a
+    # second stream inside the graph was measured slower (fork/join cost > the ~2 us fill).
     graph = None
     G = 100
     if args.graph:
@@ -217,7 +240,10 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "v1_step_kernel<%d,float>" % n if args.kind == "v1" else "v0_step_kernel<float>",
-                     "kernel_ms": kernel_ms, "algo_bytes_per_launch": per_env * B,
+                     "kernel_ms": kernel_ms, "kernel_ms_dispatch_events": kernel_ms_dispatch,
+                     "kernel_timing": "HIP events around a hipGraph of %d back-to-back step launches"
+                                      % args.profile_steps,
+                     "algo_bytes_per_launch": per_env * B,
                      "algo_bytes_per_env_step": per_env, "traffic_source": traffic_src},
         "episodes": {"finished": float(stats[1]),
                      "mean_return": float(stats[0] / stats[1]) if stats[1] else None},

@@ -41,7 +41,7 @@ struct FutbolCtx {
     size_t state_bytes = 0;
     std::vector<Field> fields;
     double* d_spill = nullptr;
-    unsigned long long* d_invalid = nullptr;  // [0] invalid-action count, [1] synthetic-policy step
+    unsigned long long* d_invalid = nullptr;  // [0] invalid-action count, [1] counter-driven fill launches x blocks
     V1Ptrs v1{};
     V0Ptrs v0{};
     double steps_since_clear = 0.0;
@@ -360,7 +360,6 @@ extern "C" int futbol_create(const FutbolConfig* cfg, int32_t device, uint64_t s
         s.stat_cnt = (uint32_t*)fptr("stat_cnt");
         s.spill = ctx->d_spill;
         s.invalid = ctx->d_invalid;
-        s.act_step = ctx->d_invalid + 1;
         s.stamps = nullptr;
 #ifdef FUTBOL_STAMPS
         if ((he = hipMalloc((void**)&ctx->d_stamps, (size_t)((B + 63) / 64 + 1) * 16 * 8)) != hipSuccess)
@@ -392,7 +391,6 @@ extern "C" int futbol_create(const FutbolConfig* cfg, int32_t device, uint64_t s
         s.stat_ret = (double*)fptr("stat_ret");
         s.stat_cnt = (uint32_t*)fptr("stat_cnt");
         s.invalid = ctx->d_invalid;
-        s.act_step = ctx->d_invalid + 1;
         int rc = launch_v0((const V0Params*)ctx->d_params, B, s, 0, 1, nullptr, nullptr, nullptr, nullptr, nullptr,
                            nullptr, 1, 0);
         if (rc) return bail(hipGetLastError(), "launch(init)");
@@ -518,7 +516,7 @@ extern "C" int futbol_fill_actions(FutbolCtx* ctx, uint64_t seed, uint64_t step,
     FB_CHECK_HIP(ctx, hipSetDevice(ctx->device));
     int nvals = 5;  // MultiDiscrete([5, 5] * N) (envs_v1/futbol_env.py:78-79)
     if (ctx->cfg.env_kind == FUTBOL_ENV_V0) nvals = ctx->cfg.action_as_int0 ? 16 : 4;  // Discrete(16) / Tuple(4, 4)
-    const unsigned long long* ctr = step == ~(uint64_t)0 ? ctx->d_invalid + 1 : nullptr;
+    unsigned long long* ctr = step == ~(uint64_t)0 ? ctx->d_invalid + 1 : nullptr;
     if (launch_fill_actions(seed, step, ctr, (uint32_t)ctx->env_base, ctx->B, ctx->act_dim, nvals, actions,
                             (hipStream_t)stream))
         return fail(ctx, FUTBOL_EHIP, "fill_actions launch failed");

@@ -7,21 +7,28 @@
 namespace futbol {
 
 // actions[i][j] = floor(U * nvals), U = draw j of (seed, env_base + i, event = step, tag 1):
-// the benchmark's "left agent" (random_action() for the left team, envs_v1/futbol_env.py:306-307)
-// step_ctr != nullptr: use the device counter (advanced by every step launch) instead of `step`,
-// so a captured hipGraph draws fresh actions at every replay.
-__global__ void __launch_bounds__(256) fill_actions_kernel(uint64_t seed, uint32_t step, const unsigned long long* step_ctr,
+// the benchmark's "left agent" (random_action() for the left team, envs_v1/futbol_env.py:306-307).
+// fill_ctr != nullptr: the step is this launch's index among the context's counter-driven fills
+// (0, 1, 2, ...): every block adds 1 to the counter and divides the old value by the grid size,
+// which is exact because such launches are stream-ordered among themselves.  The counter is
+// independent of the step kernel, so a fill can run on a second stream concurrently with a step,
+// and a captured hipGraph draws fresh actions at every replay.
+__global__ void __launch_bounds__(256) fill_actions_kernel(uint64_t seed, uint32_t step, unsigned long long* fill_ctr,
                                                            uint32_t env_base, int B, int adim, int nvals,
                                                            uint8_t* __restrict__ actions)
 {
+    __shared__ uint32_t s_step;
+    if (fill_ctr) {
+        if (threadIdx.x == 0) s_step = (uint32_t)(atomicAdd(fill_ctr, 1ull) / gridDim.x);
+        __syncthreads();
+    }
     const int env = blockIdx.x * blockDim.x + threadIdx.x;
     if (env >= B) return;
-    const uint32_t s = step_ctr ? (uint32_t)*step_ctr : step;
+    const uint32_t s = fill_ctr ? s_step : step;
     Stream rs(seed, env_base + (uint32_t)env, s, 1);
     for (int j = 0; j < adim; ++j) actions[(size_t)env * adim + j] = (uint8_t)rs.choice(nvals);
 }
-
-int launch_fill_actions(uint64_t seed, uint64_t step, const unsigned long long* step_ctr, uint32_t env_base, int B,
+int launch_fill_actions(uint64_t seed, uint64_t step, unsigned long long* step_ctr, uint32_t env_base, int B,
                         int adim, int nvals, uint8_t* actions, hipStream_t stream)
 {
     hipLaunchKernelGGL(fill_actions_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, seed, (uint32_t)step,

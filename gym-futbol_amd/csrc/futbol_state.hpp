@@ -62,7 +62,6 @@ struct V1Ptrs {
     uint32_t* stat_cnt;
     double* spill;        // contact records beyond the LDS capacity: [P][8][B]
     unsigned long long* invalid;  // count of clamped out-of-range actions
-    unsigned long long* act_step; // synthetic-policy step counter, +1 per step launch
     unsigned long long* stamps;   // diagnostic builds only (FUTBOL_STAMPS): [blocks][16] cycle sums
 };
 
@@ -75,7 +74,6 @@ struct V0Ptrs {
     double* stat_ret;
     uint32_t* stat_cnt;
     unsigned long long* invalid;
-    unsigned long long* act_step;
 };
 
 }  // namespace futbol

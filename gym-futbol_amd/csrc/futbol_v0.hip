@@ -487,7 +487,6 @@ __global__ void __launch_bounds__(64) v0_step_kernel(const V0Params* __restrict_
     reward[env] = (OT)rw;
     done_out[env] = done ? 1 : 0;
     store(st, env, B, e, m, row_valid);
-    if (env == 0) *st.act_step += 1;
 }
 
 template <typename OT>

@@ -916,7 +916,6 @@ __global__ void __launch_bounds__(EPW) v1_step_kernel(const V1Params* __restrict
     done_out[env] = done ? 1 : 0;
     store_env<N>(st, env, B, e);
     FUTBOL_STAMP(10);
-    if (env == 0) *st.act_step += 1;  // stream-ordered after this step's fill_actions
 }
 
 // futbol_create (init=1: Futbol.__init__, which ends in reset()) / futbol_reset (masked)

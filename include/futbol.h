@@ -97,9 +97,11 @@ int futbol_step(FutbolCtx* ctx, const uint8_t* actions, void* obs, void* reward,
                 void* terminal_obs, void* stream);
 
 /* Synthetic policy: actions[i] = iid uniform action of env (env_id_base+i) at
-   `step` from the tag-1 Philox stream keyed by `seed`.  step == UINT64_MAX: use
-   the context's device step counter instead (it advances by one at every
-   futbol_step launch), so a captured hipGraph draws fresh actions per replay. */
+   `step` from the tag-1 Philox stream keyed by `seed`.  step == UINT64_MAX: the
+   step is the number of earlier UINT64_MAX calls on this context (0, 1, 2, ...),
+   counted on the device, so a captured hipGraph draws fresh actions per replay.
+   The counter is independent of futbol_step: a fill may run on another stream
+   concurrently with a step (double-buffered actions). */
 int futbol_fill_actions(FutbolCtx* ctx, uint64_t seed, uint64_t step, uint8_t* actions, void* stream);
 
 /* Episode statistics since the last clear: out3 (device, f64[3]) =

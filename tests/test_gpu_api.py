@@ -211,6 +211,9 @@ def test_random_actions_follow_the_tape(kind, kw, nvals):
         exp = np.array([[synthetic_action(99, base + i, step, j, nvals) for j in range(venv.action_dim)]
                         for i in range(B)])
         assert np.array_equal(a, exp)
+    for k in range(3):   # counter-driven fills: the k-th such call draws step k
+        a = venv.random_actions(2**64 - 1, seed=99).cpu().numpy()
+        assert np.array_equal(a, venv.random_actions(k, seed=99, out=torch.empty_like(venv._act)).cpu().numpy())
     venv.close()
 
 
