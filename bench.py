@@ -102,12 +102,38 @@ def stamps_report(venv, one_step, args):
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     nat.check(nat.load().futbol_debug_stamps(venv.ctx.h, buf.ctypes.data, buf.size, 0), venv.ctx.h)
-    epw = int(os.environ.get("FUTBOL_EPW", "64"))
+    epw = 64
     per = buf[:nblk * 16].reshape(nblk, 16).astype(np.float64).sum(0) / (nblk * steps * (64 // epw))  # per wave
     tot = per[:11].sum()
     rep = {"diagnostic": "stamps", "envs_per_wave": epw, "steps": steps, "ms_per_step_wall": wall / steps * 1e3,
            "cycles_per_wave_step_total": tot,
-           "phases": {STAMP_SLOTS[i]: {"cycles": per[i], "share": per[i] / tot} for i in range(11)}}
+           "phases": {STAMP_SLOTS[i]: {"cycles": per[i], "share": per[i] / tot} for i in range(11)},
+           "solver_records_per_wave_step": per[15]}
+    # single-launch snapshots: wave start/end (100 MHz realtime), cycles, placement
+    snaps = []
+    slow = np.zeros(16)
+    for k in range(args.snapshots):
+        for _ in range(args.snapshot_stride - 1):
+            one_step()
+        nat.check(nat.load().futbol_debug_stamps(venv.ctx.h, buf.ctypes.data, buf.size, 1), venv.ctx.h)  # clear
+        one_step()
+        torch.cuda.synchronize()
+        nat.check(nat.load().futbol_debug_stamps(venv.ctx.h, buf.ctypes.data, buf.size, 0), venv.ctx.h)
+        w = buf[:nblk * 16].reshape(nblk, 16)
+        slow += w[int(np.argmax(w[:, 13]))].astype(np.float64)   # phases of this launch's slowest wave
+        t0_, t1_, cyc, hw = (w[:, 11].astype(np.float64), w[:, 12].astype(np.float64),
+                             w[:, 13].astype(np.float64), w[:, 14])
+        place = (hw >> np.uint64(32)) * np.uint64(1 << 12) + ((hw >> np.uint64(4)) & np.uint64(0xFFF))
+        _, per_simd = np.unique(place, return_counts=True)
+        dur = (t1_ - t0_) / 100.0
+        snaps.append({"span_us": (t1_.max() - t0_.min()) / 100.0, "start_spread_us": (t0_.max() - t0_.min()) / 100.0,
+                      "wave_us_mean": dur.mean(), "wave_us_p90": float(np.percentile(dur, 90)), "wave_us_max": dur.max(),
+                      "wave_cycles_mean": cyc.mean(), "wave_cycles_max": cyc.max(),
+                      "simds_used": int(len(per_simd)), "max_waves_per_simd": int(per_simd.max())})
+    rep["slowest_wave_phases"] = {STAMP_SLOTS[i]: slow[i] / max(len(snaps), 1) for i in range(11)}
+    rep["slowest_wave_records"] = slow[15] / max(len(snaps), 1)
+    rep["snapshots"] = snaps
+    rep["snapshot_mean"] = {k: float(np.mean([x[k] for x in snaps])) for k in snaps[0]} if snaps else None
     print(json.dumps(rep, indent=1))
     venv.close()
 
@@ -124,6 +150,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=600,
                     help="steps timed per-kernel with HIP events (a multiple of the episode length)")
+    ap.add_argument("--snapshots", type=int, default=24, help="--stamps: single-launch wave snapshots")
+    ap.add_argument("--snapshot-stride", type=int, default=5, help="--stamps: steps between snapshots")
     ap.add_argument("--stamps", action="store_true",
                     help="diagnostic: load the FUTBOL_STAMPS build and print the per-phase cycle breakdown")
     args = ap.parse_args()

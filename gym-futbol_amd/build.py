@@ -16,7 +16,9 @@ from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-CSRC = os.path.join(HERE, "csrc")
+# A/B experiments: FUTBOL_CSRC=<other source tree> FUTBOL_BUILD_VARIANT=<name> builds
+# gym_futbol_amd/libfutbol_amd_<name>.so, loaded with FUTBOL_LIB_VARIANT=<name>
+CSRC = os.environ.get("FUTBOL_CSRC", os.path.join(HERE, "csrc"))
 VARIANT = os.environ.get("FUTBOL_BUILD_VARIANT", "")  # "stamps": diagnostic build with -DFUTBOL_STAMPS
 OBJ = os.path.join(HERE, "build", "obj" + ("_" + VARIANT if VARIANT else ""))
 LIB = os.path.join(HERE, "gym_futbol_amd", "libfutbol_amd%s.so" % ("_" + VARIANT if VARIANT else ""))

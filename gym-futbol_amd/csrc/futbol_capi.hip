@@ -11,6 +11,7 @@
 #include <vector>
 #include "../../include/futbol.h"
 #include "futbol_kernels.hpp"
+#include "futbol_v1_params.hpp"
 #include "futbol_rng.hpp"
 
 using namespace futbol;
@@ -35,7 +36,8 @@ struct FutbolCtx {
     int device = 0;
     uint64_t seed = 0, env_base = 0;
     int B = 0, N = 0, obs_dim = 0, act_dim = 0, K_done = 0;
-    int epw = 64;  // envs per one-wave block of the v1 kernels (FUTBOL_EPW=32 to override)
+    int epw = 64;     // envs per one-wave block of the v1 kernels
+    int v1_def = 0;   // the default-field (compile-time geometry) kernel applies
     void* d_params = nullptr;
     char* d_state = nullptr;
     size_t state_bytes = 0;
@@ -97,21 +99,6 @@ extern "C" int futbol_config_default(int32_t env_kind, int32_t number_of_player,
 }
 
 // Team._create_pos_array (team.py:52-112), player k of a team
-static void formation(int N, double W, double H, int side, int k, double* x, double* y)
-{
-    if (N <= 3) {
-        *x = side == 0 ? W * 0.25 : W * 0.75;
-        *y = (H / (double)(N + 1)) * (double)(k + 1);
-    } else if (N <= 6) {
-        if (k < 3) { *x = side == 0 ? (W * 1) / 6 : (W * 5) / 6; *y = (H / 4.0) * (double)(k + 1); }
-        else { *x = side == 0 ? (W * 2) / 6 : (W * 4) / 6; *y = (H / (double)(N - 3 + 1)) * (double)(k - 3 + 1); }
-    } else {
-        if (k < 4) { *x = side == 0 ? (W * 1) / 8 : (W * 7) / 8; *y = (H / 5.0) * (double)(k + 1); }
-        else if (k < 7) { *x = side == 0 ? (W * 2) / 8 : (W * 6) / 8; *y = (H / 4.0) * (double)(k - 4 + 1); }
-        else { *x = side == 0 ? (W * 3) / 8 : (W * 5) / 8; *y = (H / (double)(N - 7 + 1)) * (double)(k - 7 + 1); }
-    }
-}
-
 // largest double s with RN(sqrt(s)) <= vmax: `sqrt(s) > vmax` <=> `s > T` (sqrt is correctly
 // rounded, hence monotone), which lets the kernel skip the sqrt of limit_velocity when no clamp happens
 static double clamp_threshold(double vmax)
@@ -137,59 +124,17 @@ static bool bbt_consistent(const V1Params* p)
 
 static int fill_v1_params(const FutbolConfig* c, uint64_t seed, uint64_t env_base, int B, int K_done, V1Params* p)
 {
-    memset(p, 0, sizeof(*p));
-    const double W = c->width, H = c->height, G = 20.0;  // GOAL_SIZE (envs_v1/futbol_env.py:21)
-    p->W = W;
-    p->H = H;
-    const double lo = H / 2 - G / 2, hi = H / 2 + G / 2;
-    // _setup_walls (envs_v1/futbol_env.py:182-234): 6 walls then 6 goal-box segments
-    const double seg[12][4] = {{0, 0, 0, lo},       {0, hi, 0, H},          {0, H, W, H},
-                               {W, 0, W, lo},       {W, hi, W, H},          {0, 0, W, 0},
-                               {-2, lo, -2, hi},    {-2, lo, 0, lo},        {-2, hi, 0, hi},
-                               {W + 2, lo, W + 2, hi}, {W, lo, W + 2, lo}, {W, hi, W + 2, hi}};
-    for (int s = 0; s < 12; ++s) {
-        p->sax[s] = seg[s][0];
-        p->say[s] = seg[s][1];
-        p->sbx[s] = seg[s][2];
-        p->sby[s] = seg[s][3];
-        // cpSegmentShapeCacheData: bb = (min - r, ..., max + r), r = 1
-        const double l = seg[s][0] < seg[s][2] ? seg[s][0] : seg[s][2];
-        const double r = seg[s][0] < seg[s][2] ? seg[s][2] : seg[s][0];
-        const double b = seg[s][1] < seg[s][3] ? seg[s][1] : seg[s][3];
-        const double t = seg[s][1] < seg[s][3] ? seg[s][3] : seg[s][1];
-        p->sl[s] = l - 1.0;
-        p->sb[s] = b - 1.0;
-        p->sr[s] = r + 1.0;
-        p->st[s] = t + 1.0;
-        const double sdx = seg[s][2] - seg[s][0], sdy = seg[s][3] - seg[s][1];
-        p->L2[s] = sdx * sdx + sdy * sdy;
-        p->rL2[s] = 1.0 / p->L2[s];
-    }
-    // distinct BB bounds, segment by segment as used by the kernel's candidate test
-    BBT& T = p->bbt;
-    T.r1 = p->sr[0]; T.rW1 = p->sr[2]; T.rm1 = p->sr[6]; T.rW3 = p->sr[9];
-    T.lm1 = p->sl[0]; T.lW1 = p->sl[3]; T.lm3 = p->sl[6]; T.lWp1 = p->sl[9];
-    T.tlo = p->st[0]; T.tH = p->st[1]; T.t1 = p->st[5]; T.thi = p->st[6];
-    T.bm1 = p->sb[0]; T.bhi = p->sb[1]; T.bH = p->sb[2]; T.blo = p->sb[6];
-    const int N = c->number_of_player;
-    for (int side = 0; side < 2; ++side)
-        for (int k = 0; k < N; ++k) formation(N, W, H, side, k, &p->fx[side * N + k], &p->fy[side * N + k]);
-    p->fx[2 * N] = W * 0.5;  // Ball(width*0.5, height*0.5) (envs_v1/futbol_env.py:122,135)
-    p->fy[2 * N] = H * 0.5;
-    // cpSpace defaults (Chipmunk 7 cpSpaceInit): collisionSlop 0.1f, collisionBias cpfpow(1.0f - 0.1f, 60.0f);
-    // damping 0.95 (envs_v1/futbol_env.py:99); dt 0.1 (TIME_STEP) and 1e-4 (_position_to_initial)
+    // cpSpace defaults (Chipmunk 7 cpSpaceInit): collisionBias cpfpow(1.0f - 0.1f, 60.0f);
+    // damping 0.95 (envs_v1/futbol_env.py:99) over dt 1e-4 and 0.1
     const double cbias = pow((double)(1.0f - 0.1f), 60.0);
-    p->dtv[0] = 0.0;
-    p->dtv[1] = 0.0001;
-    p->dtv[2] = 0.1;
-    for (int i = 1; i < 3; ++i) {
-        p->damp[i] = pow(0.95, p->dtv[i]);
-        p->biasc[i] = 1.0 - pow(cbias, p->dtv[i]);
-        p->rdt[i] = 1.0 / p->dtv[i];
-    }
-    p->slop = (double)0.1f;
-    p->clamp2_player = clamp_threshold(10.0);  // PLAYER_MAX_VELOCITY
-    p->clamp2_ball = clamp_threshold(25.0);    // BALL_MAX_VELOCITY
+    V1Pow pw{};
+    pw.damp1 = pow(0.95, 0.0001);
+    pw.damp2 = pow(0.95, 0.1);
+    pw.biasc1 = 1.0 - pow(cbias, 0.0001);
+    pw.biasc2 = 1.0 - pow(cbias, 0.1);
+    pw.clamp2_player = clamp_threshold(10.0);  // PLAYER_MAX_VELOCITY
+    pw.clamp2_ball = clamp_threshold(25.0);    // BALL_MAX_VELOCITY
+    *p = v1_params_geometry(c->number_of_player, c->width, c->height, pw);
     p->seed = seed;
     p->env_base = (uint32_t)env_base;
     p->B = B;
@@ -342,6 +287,9 @@ extern "C" int futbol_create(const FutbolConfig* cfg, int32_t device, uint64_t s
             futbol_destroy(ctx);
             return fail(nullptr, FUTBOL_EINVAL, "segment bounding boxes inconsistent (width/height)");
         }
+        // FUTBOL_GENERIC=1 forces the runtime-geometry kernel (tests compare both instances)
+        const char* gen = getenv("FUTBOL_GENERIC");
+        ctx->v1_def = (gen && atoi(gen)) ? 0 : (v1_is_default_geometry(N, hp) ? 1 : 0);
         if ((he = hipMalloc(&ctx->d_params, sizeof(V1Params))) != hipSuccess) return bail(he, "hipMalloc(params)");
         if ((he = hipMemcpy(ctx->d_params, &hp, sizeof(hp), hipMemcpyHostToDevice)) != hipSuccess)
             return bail(he, "hipMemcpy(params)");
@@ -368,12 +316,7 @@ extern "C" int futbol_create(const FutbolConfig* cfg, int32_t device, uint64_t s
             return bail(he, "hipMemset(stamps)");
         s.stamps = ctx->d_stamps;
 #endif
-        if (const char* ev = getenv("FUTBOL_EPW")) ctx->epw = atoi(ev);
-        if (!v1_supported_epw(ctx->epw)) {
-            futbol_destroy(ctx);
-            return fail(nullptr, FUTBOL_EINVAL, "FUTBOL_EPW must be 64 or 32");
-        }
-        int rc = launch_v1(N, ctx->epw, (const V1Params*)ctx->d_params, B, s, 0, 1, nullptr, nullptr, nullptr,
+        int rc = launch_v1(N, ctx->epw, ctx->v1_def, (const V1Params*)ctx->d_params, B, s, 0, 1, nullptr, nullptr, nullptr,
                            nullptr, nullptr, nullptr, 1, 0);
         if (rc) return bail(hipGetLastError(), "launch(init)");
     } else {
@@ -481,7 +424,7 @@ static int launch(FutbolCtx* ctx, int what, const uint8_t* actions, const uint8_
     }
     int rc;
     if (ctx->cfg.env_kind == FUTBOL_ENV_V1)
-        rc = launch_v1(ctx->N, ctx->epw, (const V1Params*)ctx->d_params, ctx->B, ctx->v1, out64, what, actions,
+        rc = launch_v1(ctx->N, ctx->epw, ctx->v1_def, (const V1Params*)ctx->d_params, ctx->B, ctx->v1, out64, what, actions,
                        mask, obs, reward, done, term, 0, (hipStream_t)stream);
     else
         rc = launch_v0((const V0Params*)ctx->d_params, ctx->B, ctx->v0, out64, what, actions, mask, obs, reward,

@@ -71,12 +71,13 @@ inline void launch_kernel(void (*k)(KArgs...), dim3 grid, dim3 block, hipStream_
 }
 
 // P: device pointer to the context's V1Params (wave-uniform scalar loads)
-int launch_v1(int N, int epw, const V1Params* P, int B, const V1Ptrs& st, int out64, int what,
+int launch_v1(int N, int epw, int def, const V1Params* P, int B, const V1Ptrs& st, int out64, int what,
               const uint8_t* actions, const uint8_t* mask, void* obs, void* reward, uint8_t* done, void* term,
               int init, hipStream_t stream);
 int v1_supported(int N);
 int v1_supported_epw(int epw);
 size_t v1_spill_slots(int N);
+bool v1_is_default_geometry(int N, const V1Params& p);
 
 int launch_v0(const V0Params* P, int B, const V0Ptrs& st, int out64, int what, const uint8_t* actions,
               const uint8_t* mask, void* obs, void* reward, uint8_t* done, void* term, int init,

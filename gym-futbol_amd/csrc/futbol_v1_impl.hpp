@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "futbol_kernels.hpp"
+#include "futbol_v1_params.hpp"
 #include "futbol_rng.hpp"
 #include "futbol_state.hpp"
 #include "futbol_util.hpp"
@@ -65,18 +66,20 @@ struct V1Shape {
     static constexpr int Nb = 2 * N + 1;
     static constexpr int BALL = 2 * N;
     static constexpr int P = v1_npairs(N);
-    // LDS slots per lane for contact records: 4 one-wave blocks per CU fit in 160 KB
-    static constexpr int K = N <= 2 ? 7 : (N <= 5 ? 4 : 2);
+    // LDS contact-record slots per lane: 4 one-wave blocks per CU must fit in 160 KB
+    // (40 KB per block: K * 4 KB of records + (2 Nb + 1) KB of solver velocity rows + the segment table)
+    static constexpr int K = N == 1 ? 8 : (N == 2 ? 7 : (N == 3 ? 6 : (N == 5 ? 4 : 2)));
 };
 
 __device__ __forceinline__ double minv_of(int k, int ball) { return k == ball ? kBallMinv : kPlayerMinv; }
 
-// correctly rounded x / c for a constant c with rc = RN(1/c)
+// correctly rounded x / c for a constant c > 0 with rc = RN(1/c).  x = +-0 returns x * rc
+// (the correction step would turn -0 into +0)
 __device__ __forceinline__ double cdiv(double x, double c, double rc)
 {
     const double q0 = x * rc;
     const double r = __builtin_fma(-q0, c, x);
-    return __builtin_fma(r, rc, q0);
+    return x == 0.0 ? q0 : __builtin_fma(r, rc, q0);
 }
 
 struct SegLds {
@@ -89,19 +92,43 @@ struct SegLds {
 template <int N, int EPW>
 struct Scratch {
     using S = V1Shape<N>;
-    static constexpr int K = S::K * (64 / EPW);  // LDS contact slots per lane
+    // LDS contact slots per lane: the same at every EPW, so that 64/EPW times as many blocks fit per CU
+    static constexpr int K = S::K;
     // contact record s of lane l: rec[s][0][l] = (nx, ny), [1] = (nMass, bias),
     // [2] = (bounce, info bits), [3] = (jnAcc, jBias): four ds_read_b128 per record
     double2 rec[K][4][EPW];
-    double2 v[S::Nb][EPW];   // body velocity during the solve
-    double2 vb[S::Nb][EPW];  // body v_bias during the solve
+    // body velocity / v_bias during the solve; v row Nb is the static body (segments) and
+    // the target of null records: it stays exactly +0.0 (its inverse mass is 0), and it also
+    // serves as the static body's v_bias row (vrow_of / brow_of)
+    double2 v[S::Nb + 1][EPW];
+    double2 vb[S::Nb][EPW];
     SegLds seg[kNSeg];
 };
 
-// info word: a (5 bits) | bcode (6 bits: body id, or 32 + segment) << 5 | pair << 11 | normal << 20
-__device__ __forceinline__ int pack_info(int a, int bcode, int pair, bool normal)
+// info word (64 bits, stored as the bits of a double):
+//   low 32: a (5 bits) | bcode (6 bits: body id, or 32 + segment) << 5 | pair << 11 | normal << 20
+//   high 32: byte offset of a's solver row | byte offset of b's row (static row for segments) << 16,
+//            filled in by with_rows() in the solver prologue (not at the many collide sites:
+//            constants hoisted out of them cost registers)
+__device__ __forceinline__ long long pack_info(int a, int bcode, int pair, bool normal)
 {
-    return a | (bcode << 5) | (pair << 11) | ((normal ? 1 : 0) << 20);
+    return (long long)(uint32_t)(a | (bcode << 5) | (pair << 11) | ((normal ? 1 : 0) << 20));
+}
+template <int N, int EPW>
+__device__ __forceinline__ long long with_rows(long long info)
+{
+    constexpr uint32_t ROW = EPW * (uint32_t)sizeof(double2);
+    const uint32_t lo = (uint32_t)info;
+    const uint32_t a = lo & 31u, bcode = (lo >> 5) & 63u;
+    const uint32_t b = bcode < 32u ? bcode : (uint32_t)V1Shape<N>::Nb;
+    return (long long)(((unsigned long long)((a * ROW) | ((b * ROW) << 16)) << 32) | lo);
+}
+// null record (slots between a lane's contact count and the wave's): both rows static
+template <int N, int EPW>
+__device__ __forceinline__ long long null_info()
+{
+    constexpr uint32_t R = (uint32_t)(V1Shape<N>::Nb * EPW * (int)sizeof(double2));
+    return (long long)(((unsigned long long)(R | (R << 16)) << 32));
 }
 
 // global spill record (slot s >= K): 8 doubles [nx, ny, nMass, bias, bounce, info, jnAcc, jBias]
@@ -133,47 +160,49 @@ struct Lane {
     __device__ __forceinline__ int get_info(int s) const { return (int)__double_as_longlong(get(s, 2).y); }
     __device__ __forceinline__ double get_jn(int s) const { return get(s, 3).x; }
     __device__ __forceinline__ void set_rec(int s, double nx, double ny, double nm, double bi, double bo, double j,
-                                            int info) const
+                                            long long info) const
     {
         put(s, 0, make_double2(nx, ny));
         put(s, 1, make_double2(nm, bi));
-        put(s, 2, make_double2(bo, __longlong_as_double((long long)info)));
+        put(s, 2, make_double2(bo, __longlong_as_double(info)));
         put(s, 3, make_double2(j, 0.0));
     }
 };
 
-// One contact of cpArbiterApplyImpulse (frictionless), record and body velocities in
-// LDS (FAST: slot < K, no branches) or the record in the global spill area.
-template <int N, int EPW, bool FAST>
-__device__ __forceinline__ void solve_contact(const Lane<N, EPW>& L, int s)
+// LDS address of a solver row from its byte offset (info): v rows directly, v_bias rows with
+// the static offset redirected to the (zero) static v row
+template <int N, int EPW>
+__device__ __forceinline__ double2* vrow_of(Scratch<N, EPW>* sh, int ln, uint32_t off)
+{
+    return (double2*)((char*)&sh->v[0][ln] + off);
+}
+template <int N, int EPW>
+__device__ __forceinline__ double2* brow_of(Scratch<N, EPW>* sh, int ln, uint32_t off)
+{
+    constexpr uint32_t SROW = (uint32_t)V1Shape<N>::Nb * EPW * (uint32_t)sizeof(double2);
+    return off == SROW ? &sh->v[V1Shape<N>::Nb][ln] : (double2*)((char*)&sh->vb[0][ln] + off);
+}
+
+// One contact of cpArbiterApplyImpulse (frictionless).  r0..r2 = the record's constant
+// part (normal, nMass, bias, bounce, info), r3 = (jnAcc, jBias), written back to *r3p.
+// Body rows come from the info offsets; a segment's b is the static row (v = v_bias = 0,
+// inverse mass 0: its updates add +-0 to +0 and leave it +0), which reproduces
+// Chipmunk's static-body arithmetic exactly without a branch.
+template <int N, int EPW>
+__device__ __forceinline__ void apply_contact(Scratch<N, EPW>* sh, int ln, double2 r0, double2 r1, double2 r2,
+                                              double2 r3, double2* r3p)
 {
     using S = V1Shape<N>;
-    Scratch<N, EPW>* sh = L.sh;
-    const int ln = L.lane;
-    double2 r0, r1, r2, r3;
-    if constexpr (FAST) {
-        r0 = sh->rec[s][0][ln];
-        r1 = sh->rec[s][1][ln];
-        r2 = sh->rec[s][2][ln];
-        r3 = sh->rec[s][3][ln];
-    } else {
-        r0 = L.get(s, 0);
-        r1 = L.get(s, 1);
-        r2 = L.get(s, 2);
-        r3 = L.get(s, 3);
-    }
-    const int info = (int)__double_as_longlong(r2.y);
-    const int a = info & 31, bcode = (info >> 5) & 63;
-    const bool dyn = bcode < 32;
-    const int b = dyn ? bcode : a;  // any valid slot; masked by dyn below
+    constexpr uint32_t ROW = EPW * (uint32_t)sizeof(double2);
+    const uint32_t offs = (uint32_t)((unsigned long long)__double_as_longlong(r2.y) >> 32);
+    const uint32_t ao = offs & 0xffffu, bo = offs >> 16;
+    double2* pva = vrow_of(sh, ln, ao);
+    double2* pvb = vrow_of(sh, ln, bo);
+    double2* pba = brow_of(sh, ln, ao);
+    double2* pbb = brow_of(sh, ln, bo);
+    const double2 va = *pva, ba = *pba, vbv = *pvb, bbv = *pbb;
     const double nx = r0.x, ny = r0.y, nMass = r1.x, bias = r1.y, bounce = r2.x;
     const double jnOld = r3.x, jbOld = r3.y;
-    const double2 va = sh->v[a][ln], ba = sh->vb[a][ln];
-    double2 vbv = sh->v[b][ln], bbv = sh->vb[b][ln];
-    if (!dyn) {
-        vbv = make_double2(0.0, 0.0);
-        bbv = make_double2(0.0, 0.0);
-    }
     const double vbn = (bbv.x - ba.x) * nx + (bbv.y - ba.y) * ny;
     const double vrn = (vbv.x - va.x) * nx + (vbv.y - va.y) * ny;
     const double jbn = (bias - vbn) * nMass;
@@ -182,43 +211,101 @@ __device__ __forceinline__ void solve_contact(const Lane<N, EPW>& L, int s)
     const double jnv = -(bounce + vrn) * nMass;
     const double tn = jnOld + jnv;
     const double jnAcc = tn > 0.0 ? tn : 0.0;
-    if constexpr (FAST) sh->rec[s][3][ln] = make_double2(jnAcc, jb);
-    else L.put(s, 3, make_double2(jnAcc, jb));
+    *r3p = make_double2(jnAcc, jb);
     const double db = jb - jbOld, dj = jnAcc - jnOld;
     const double jbx = nx * db, jby = ny * db, jx = nx * dj, jy = ny * dj;
-    const double ma = minv_of(a, S::BALL);
-    sh->vb[a][ln] = make_double2(ba.x + (-jbx) * ma, ba.y + (-jby) * ma);
-    sh->v[a][ln] = make_double2(va.x + (-jx) * ma, va.y + (-jy) * ma);
-    if (dyn) {
-        const double mb = minv_of(b, S::BALL);
-        sh->vb[b][ln] = make_double2(bbv.x + jbx * mb, bbv.y + jby * mb);
-        sh->v[b][ln] = make_double2(vbv.x + jx * mb, vbv.y + jy * mb);
-    }
+    const double ma = ao == (uint32_t)S::BALL * ROW ? kBallMinv : kPlayerMinv;
+    const double mb = bo == (uint32_t)S::BALL * ROW ? kBallMinv : (bo == (uint32_t)S::Nb * ROW ? 0.0 : kPlayerMinv);
+    *pba = make_double2(ba.x + (-jbx) * ma, ba.y + (-jby) * ma);
+    *pva = make_double2(va.x + (-jx) * ma, va.y + (-jy) * ma);
+    *pbb = make_double2(bbv.x + jbx * mb, bbv.y + jby * mb);
+    *pvb = make_double2(vbv.x + jx * mb, vbv.y + jy * mb);
 }
 
 // cpArbiterApplyCachedImpulse for one contact (only NORMAL arbiters are warm started)
-template <int N, int EPW, bool FAST>
-__device__ __forceinline__ void warm_contact(const Lane<N, EPW>& L, int s, double dt_coef)
+template <int N, int EPW>
+__device__ __forceinline__ void warm_contact(Scratch<N, EPW>* sh, int ln, double2 r0, double2 r2, double2 r3,
+                                             double dt_coef)
 {
     using S = V1Shape<N>;
-    Scratch<N, EPW>* sh = L.sh;
-    const int ln = L.lane;
-    const double2 r0 = FAST ? sh->rec[s][0][ln] : L.get(s, 0);
-    const double2 r2 = FAST ? sh->rec[s][2][ln] : L.get(s, 2);
-    const double2 r3 = FAST ? sh->rec[s][3][ln] : L.get(s, 3);
-    const int info = (int)__double_as_longlong(r2.y);
+    constexpr uint32_t ROW = EPW * (uint32_t)sizeof(double2);
+    const unsigned long long info = (unsigned long long)__double_as_longlong(r2.y);
     if (!((info >> 20) & 1)) return;
-    const int a = info & 31, bcode = (info >> 5) & 63;
+    const uint32_t offs = (uint32_t)(info >> 32);
+    const uint32_t ao = offs & 0xffffu, bo = offs >> 16;
+    double2* pva = vrow_of(sh, ln, ao);
+    double2* pvb = vrow_of(sh, ln, bo);
     const double jn = r3.x;
     const double jx = (r0.x * jn) * dt_coef, jy = (r0.y * jn) * dt_coef;
-    const double ma = minv_of(a, S::BALL);
-    const double2 va = sh->v[a][ln];
-    sh->v[a][ln] = make_double2(va.x + (-jx) * ma, va.y + (-jy) * ma);
-    if (bcode < 32) {
-        const double mb = minv_of(bcode, S::BALL);
-        const double2 vbb = sh->v[bcode][ln];
-        sh->v[bcode][ln] = make_double2(vbb.x + jx * mb, vbb.y + jy * mb);
+    const double ma = ao == (uint32_t)S::BALL * ROW ? kBallMinv : kPlayerMinv;
+    const double mb = bo == (uint32_t)S::BALL * ROW ? kBallMinv : (bo == (uint32_t)S::Nb * ROW ? 0.0 : kPlayerMinv);
+    const double2 va = *pva;
+    *pva = make_double2(va.x + (-jx) * ma, va.y + (-jy) * ma);
+    const double2 vbb = *pvb;
+    *pvb = make_double2(vbb.x + jx * mb, vbb.y + jy * mb);
+}
+
+// Register-resident form of apply_contact: the record's fields are scalars held across the
+// 10 iterations, only the body rows go through LDS.  DYN = false: b is the static row
+// (segment contact or null record) -- b's velocities are exactly +0 and stay so, hence
+// they are neither read nor written; the arithmetic is the DYN = true one with b = 0.
+template <int N, int EPW, bool DYN>
+__device__ __forceinline__ void apply_rows(Scratch<N, EPW>* sh, int ln, double nx, double ny, double nMass,
+                                           double bias, double bounce, uint32_t ao, uint32_t bo, double& jnAcc,
+                                           double& jBias)
+{
+    using S = V1Shape<N>;
+    constexpr uint32_t ROW = EPW * (uint32_t)sizeof(double2);
+    double2* pva = vrow_of(sh, ln, ao);
+    double2* pba = brow_of(sh, ln, ao);
+    const double2 va = *pva, ba = *pba;
+    double2 vbv = make_double2(0.0, 0.0), bbv = make_double2(0.0, 0.0);
+    double2 *pvb = nullptr, *pbb = nullptr;
+    if constexpr (DYN) {
+        pvb = vrow_of(sh, ln, bo);
+        pbb = brow_of(sh, ln, bo);
+        vbv = *pvb;
+        bbv = *pbb;
     }
+    const double jnOld = jnAcc, jbOld = jBias;
+    const double vbn = (bbv.x - ba.x) * nx + (bbv.y - ba.y) * ny;
+    const double vrn = (vbv.x - va.x) * nx + (vbv.y - va.y) * ny;
+    const double jbn = (bias - vbn) * nMass;
+    const double tb = jbOld + jbn;
+    const double jb = tb > 0.0 ? tb : 0.0;
+    const double jnv = -(bounce + vrn) * nMass;
+    const double tn = jnOld + jnv;
+    const double jn = tn > 0.0 ? tn : 0.0;
+    jnAcc = jn;
+    jBias = jb;
+    const double db = jb - jbOld, dj = jn - jnOld;
+    const double jbx = nx * db, jby = ny * db, jx = nx * dj, jy = ny * dj;
+    const double ma = ao == (uint32_t)S::BALL * ROW ? kBallMinv : kPlayerMinv;
+    *pba = make_double2(ba.x + (-jbx) * ma, ba.y + (-jby) * ma);
+    *pva = make_double2(va.x + (-jx) * ma, va.y + (-jy) * ma);
+    if constexpr (DYN) {
+        const double mb = bo == (uint32_t)S::BALL * ROW ? kBallMinv : (bo == (uint32_t)S::Nb * ROW ? 0.0 : kPlayerMinv);
+        *pbb = make_double2(bbv.x + jbx * mb, bbv.y + jby * mb);
+        *pvb = make_double2(vbv.x + jx * mb, vbv.y + jy * mb);
+    }
+}
+
+template <int N, int EPW>
+__device__ __forceinline__ void warm_rows(Scratch<N, EPW>* sh, int ln, double nx, double ny, bool normal, uint32_t ao,
+                                          uint32_t bo, double jn, double dt_coef)
+{
+    using S = V1Shape<N>;
+    constexpr uint32_t ROW = EPW * (uint32_t)sizeof(double2);
+    if (!normal) return;
+    double2* pva = vrow_of(sh, ln, ao);
+    double2* pvb = vrow_of(sh, ln, bo);
+    const double jx = (nx * jn) * dt_coef, jy = (ny * jn) * dt_coef;
+    const double ma = ao == (uint32_t)S::BALL * ROW ? kBallMinv : kPlayerMinv;
+    const double mb = bo == (uint32_t)S::BALL * ROW ? kBallMinv : (bo == (uint32_t)S::Nb * ROW ? 0.0 : kPlayerMinv);
+    const double2 va = *pva;
+    *pva = make_double2(va.x + (-jx) * ma, va.y + (-jy) * ma);
+    const double2 vbb = *pvb;
+    *pvb = make_double2(vbb.x + jx * mb, vbb.y + jy * mb);
 }
 
 template <int N>
@@ -297,10 +384,10 @@ __device__ __forceinline__ bool cs_test(double cx, double cy, double rc, const S
     return true;
 }
 
-__device__ __forceinline__ bool cs_hit(const V1Params* __restrict__ P, int s, double cx, double cy, double rc)
+__device__ __forceinline__ bool cs_hit(const V1Params& P, int s, double cx, double cy, double rc)
 {
     double qx, qy;
-    seg_closest(cx, cy, P->sax[s], P->say[s], P->sbx[s] - P->sax[s], P->sby[s] - P->say[s], P->L2[s], P->rL2[s],
+    seg_closest(cx, cy, P.sax[s], P.say[s], P.sbx[s] - P.sax[s], P.sby[s] - P.say[s], P.L2[s], P.rL2[s],
                 qx, qy);
     const double mind = rc + kSegR;
     const double dx = qx - cx, dy = qy - cy;
@@ -317,20 +404,20 @@ __device__ __forceinline__ bool far_from_segments(double x, double y, double rea
 // ---------------------------------------------------------------------------
 // cpSpaceStep(dt) for one env.  dtc: 1 -> 1e-4, 2 -> 0.1
 template <int N, int EPW>
-__device__ __forceinline__ void space_step(const V1Params* __restrict__ P, const Lane<N, EPW>& L, Env<N>& e, int dtc
+__device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>& L, Env<N>& e, int dtc
 #ifdef FUTBOL_STAMPS
                                            , unsigned long long* st_stamps, unsigned long long& _stamp_prev
 #endif
 )
 {
     using S = V1Shape<N>;
-    const double dt = dtc == 2 ? P->dtv[2] : P->dtv[1];
-    const double rdt = dtc == 2 ? P->rdt[2] : P->rdt[1];
+    const double dt = dtc == 2 ? P.dtv[2] : P.dtv[1];
+    const double rdt = dtc == 2 ? P.rdt[2] : P.rdt[1];
     const uint32_t pc = e.meta.dtcode();
-    const double prev_dt = pc == 2 ? P->dtv[2] : (pc == 1 ? P->dtv[1] : 0.0);
-    const double biasCoef = dtc == 2 ? P->biasc[2] : P->biasc[1];
-    const double damping = dtc == 2 ? P->damp[2] : P->damp[1];
-    const double slop = P->slop, W = P->W, H = P->H;
+    const double prev_dt = pc == 2 ? P.dtv[2] : (pc == 1 ? P.dtv[1] : 0.0);
+    const double biasCoef = dtc == 2 ? P.biasc[2] : P.biasc[1];
+    const double damping = dtc == 2 ? P.damp[2] : P.damp[1];
+    const double slop = P.slop, W = P.W, H = P.H;
     e.meta.set_dtcode(dtc);
     const int B = L.B, env = L.env;
     const uint32_t ncache = e.meta.ncache();
@@ -394,7 +481,7 @@ __device__ __forceinline__ void space_step(const V1Params* __restrict__ P, const
         const bool interior = cl > 1.0 && cr < W - 1.0 && cb > 1.0 && ct < H - 1.0;
         if (!interior) {
             // cpBBIntersects(circle, segment s) for all 12 segments from the 16 distinct bounds
-            const BBT& T = P->bbt;
+            const BBT& T = P.bbt;
             const bool r1 = cl <= T.r1, rW1 = cl <= T.rW1, rm1 = cl <= T.rm1, rW3 = cl <= T.rW3;
             const bool lm1 = T.lm1 <= cr, lW1 = T.lW1 <= cr, lm3 = T.lm3 <= cr, lWp1 = T.lWp1 <= cr;
             const bool tlo = cb <= T.tlo, tH = cb <= T.tH, t1 = cb <= T.t1, thi = cb <= T.thi;
@@ -452,7 +539,7 @@ __device__ __forceinline__ void space_step(const V1Params* __restrict__ P, const
                     const double2 r2 = L.get(s, 2);
                     L.put(s, 3, make_double2(L.cjn[(size_t)c * B + env], 0.0));
                     if ((key >> 12) == 0)
-                        L.put(s, 2, make_double2(r2.x, __longlong_as_double((long long)(info | (1 << 20)))));
+                        L.put(s, 2, make_double2(r2.x, __longlong_as_double(__double_as_longlong(r2.y) | (1ll << 20))));
                     break;
                 }
             }
@@ -466,7 +553,7 @@ __device__ __forceinline__ void space_step(const V1Params* __restrict__ P, const
         e.vx[k] = e.vx[k] * damping + 0.0 * dt;
         e.vy[k] = e.vy[k] * damping + 0.0 * dt;
         const double s2 = e.vx[k] * e.vx[k] + e.vy[k] * e.vy[k];
-        const double thr = k == S::BALL ? P->clamp2_ball : P->clamp2_player;
+        const double thr = k == S::BALL ? P.clamp2_ball : P.clamp2_player;
         if (s2 > thr) {
             constexpr double vmax = k == S::BALL ? kBallVmax : kPlayerVmax;
             const double sc = vmax / sqrt(s2);
@@ -476,31 +563,118 @@ __device__ __forceinline__ void space_step(const V1Params* __restrict__ P, const
     });
 
     FUTBOL_STAMP(dtc == 2 ? 5 : 9);
-    if (n > 0) {
+    {
+        // wave-uniform record count over the LDS slots; lanes with fewer records are padded
+        // with null records, so the solver loop has no per-lane trip count
         Scratch<N, EPW>* sh = L.sh;
         const int ln = L.lane;
-        sfor<S::Nb>([&](auto K) {
-            constexpr int k = K;
-            sh->v[k][ln] = make_double2(e.vx[k], e.vy[k]);
-            sh->vb[k][ln] = make_double2(0.0, 0.0);
-        });
         constexpr int KL = Lane<N, EPW>::KL;
         const int nf = n < KL ? n : KL;  // records in LDS; slots >= KL are in the global spill
-        const double dt_coef = (prev_dt == 0.0) ? 0.0 : dt / prev_dt;
-        for (int s = 0; s < nf; ++s) warm_contact<N, EPW, true>(L, s, dt_coef);
-        for (int s = KL; s < n; ++s) warm_contact<N, EPW, false>(L, s, dt_coef);
-        for (int it = 0; it < 10; ++it) {
-            for (int s = 0; s < nf; ++s) solve_contact<N, EPW, true>(L, s);
-            for (int s = KL; s < n; ++s) solve_contact<N, EPW, false>(L, s);
+        int m = 0;
+#pragma unroll
+        for (int b = 4; b >= 0; --b) {
+            const int t = m | (1 << b);
+            if (t <= KL && __ballot(nf >= t)) m = t;
         }
-        sfor<S::Nb>([&](auto K) {
-            constexpr int k = K;
-            const double2 v = sh->v[k][ln], vb = sh->vb[k][ln];
-            e.vx[k] = v.x;
-            e.vy[k] = v.y;
-            e.bx[k] = vb.x;
-            e.by[k] = vb.y;
-        });
+        const bool spill = __ballot(n > KL) != 0;
+#ifdef FUTBOL_STAMPS
+        if ((threadIdx.x & 63) == 0 && st_stamps && dtc == 2)
+            atomicAdd(&st_stamps[(size_t)(blockIdx.x * EPW / 64) * 16 + 15], (unsigned long long)m);
+#endif
+        if (m > 0) {
+            sfor<S::Nb>([&](auto K) {
+                constexpr int k = K;
+                sh->v[k][ln] = make_double2(e.vx[k], e.vy[k]);
+                sh->vb[k][ln] = make_double2(0.0, 0.0);
+            });
+            sh->v[S::Nb][ln] = make_double2(0.0, 0.0);
+            for (int s = 0; s < nf; ++s) {
+                const double2 r2 = sh->rec[s][2][ln];
+                sh->rec[s][2][ln] = make_double2(r2.x, __longlong_as_double(with_rows<N, EPW>(__double_as_longlong(r2.y))));
+            }
+            if (spill)
+                for (int s = KL; s < n; ++s) {
+                    const double2 r2 = L.get(s, 2);
+                    L.put(s, 2, make_double2(r2.x, __longlong_as_double(with_rows<N, EPW>(__double_as_longlong(r2.y)))));
+                }
+            for (int s = nf; s < m; ++s) {
+                sh->rec[s][0][ln] = make_double2(0.0, 0.0);
+                sh->rec[s][1][ln] = make_double2(0.0, 0.0);
+                sh->rec[s][2][ln] = make_double2(0.0, __longlong_as_double(null_info<N, EPW>()));
+                sh->rec[s][3][ln] = make_double2(0.0, 0.0);
+            }
+            const double dt_coef = (prev_dt == 0.0) ? 0.0 : dt / prev_dt;
+            // the first MR slots stay in registers for the whole solve (record, jnAcc, jBias);
+            // a slot whose b is static in every lane takes the branch-free static path
+            constexpr int MR = N <= 3 ? 4 : (N <= 5 ? 3 : 2);
+            constexpr uint32_t SROW = (uint32_t)S::Nb * EPW * (uint32_t)sizeof(double2);
+            double qnx[MR], qny[MR], qnm[MR], qbi[MR], qbo[MR], qjn[MR], qjb[MR];
+            uint32_t qa[MR], qb[MR];
+            bool qnorm[MR], qdyn[MR];
+            sfor<MR>([&](auto Q) {
+                constexpr int q = Q;
+                qdyn[q] = false;
+                if (q < m) {
+                    const double2 r0 = sh->rec[q][0][ln], r1 = sh->rec[q][1][ln], r2 = sh->rec[q][2][ln],
+                                  r3 = sh->rec[q][3][ln];
+                    const unsigned long long info = (unsigned long long)__double_as_longlong(r2.y);
+                    qnx[q] = r0.x;
+                    qny[q] = r0.y;
+                    qnm[q] = r1.x;
+                    qbi[q] = r1.y;
+                    qbo[q] = r2.x;
+                    qjn[q] = r3.x;
+                    qjb[q] = r3.y;
+                    qa[q] = (uint32_t)(info >> 32) & 0xffffu;
+                    qb[q] = (uint32_t)(info >> 48);
+                    qnorm[q] = (info >> 20) & 1;
+                    qdyn[q] = __ballot(qb[q] != SROW) != 0;
+                }
+            });
+            sfor<MR>([&](auto Q) {
+                constexpr int q = Q;
+                if (q < m) warm_rows<N, EPW>(sh, ln, qnx[q], qny[q], qnorm[q], qa[q], qb[q], qjn[q], dt_coef);
+            });
+            for (int s = MR; s < m; ++s)
+                warm_contact<N, EPW>(sh, ln, sh->rec[s][0][ln], sh->rec[s][2][ln], sh->rec[s][3][ln], dt_coef);
+            if (spill)
+                for (int s = KL; s < n; ++s) warm_contact<N, EPW>(sh, ln, L.get(s, 0), L.get(s, 2), L.get(s, 3), dt_coef);
+            for (int it = 0; it < 10; ++it) {
+                sfor<MR>([&](auto Q) {
+                    constexpr int q = Q;
+                    if (q < m) {
+                        if (qdyn[q])
+                            apply_rows<N, EPW, true>(sh, ln, qnx[q], qny[q], qnm[q], qbi[q], qbo[q], qa[q], qb[q],
+                                                     qjn[q], qjb[q]);
+                        else
+                            apply_rows<N, EPW, false>(sh, ln, qnx[q], qny[q], qnm[q], qbi[q], qbo[q], qa[q], qb[q],
+                                                      qjn[q], qjb[q]);
+                    }
+                });
+                for (int s = MR; s < m; ++s)
+                    apply_contact<N, EPW>(sh, ln, sh->rec[s][0][ln], sh->rec[s][1][ln], sh->rec[s][2][ln],
+                                          sh->rec[s][3][ln], &sh->rec[s][3][ln]);
+                if (spill) {
+                    for (int s = KL; s < n; ++s) {
+                        double2 r3 = L.get(s, 3);
+                        apply_contact<N, EPW>(sh, ln, L.get(s, 0), L.get(s, 1), L.get(s, 2), r3, &r3);
+                        L.put(s, 3, r3);
+                    }
+                }
+            }
+            sfor<MR>([&](auto Q) {  // jnAcc for the arbiter cache
+                constexpr int q = Q;
+                if (q < m) sh->rec[q][3][ln] = make_double2(qjn[q], qjb[q]);
+            });
+            sfor<S::Nb>([&](auto K) {
+                constexpr int k = K;
+                const double2 v = sh->v[k][ln], vb = sh->vb[k][ln];
+                e.vx[k] = v.x;
+                e.vy[k] = v.y;
+                e.bx[k] = vb.x;
+                e.by[k] = vb.y;
+            });
+        }
     }
 
     FUTBOL_STAMP(dtc == 2 ? 6 : 9);
@@ -540,12 +714,12 @@ __device__ __forceinline__ void space_step(const V1Params* __restrict__ P, const
 
 // ---------------------------------------------------------------------------
 template <int N>
-__device__ __forceinline__ void position_to_initial(const V1Params* __restrict__ P, Env<N>& e)
+__device__ __forceinline__ void position_to_initial(const V1Params& P, Env<N>& e)
 {
     sfor<V1Shape<N>::Nb>([&](auto K) {
         constexpr int k = K;
-        e.px[k] = P->fx[k];
-        e.py[k] = P->fy[k];
+        e.px[k] = P.fx[k];
+        e.py[k] = P.fy[k];
         e.vx[k] = 0.0;
         e.vy[k] = 0.0;
     });
@@ -604,17 +778,17 @@ __device__ __forceinline__ void store_env(const V1Ptrs& st, int env, int B, cons
 
 // the block's segment table in LDS (per-lane dynamic segment index in the collide loop)
 template <int N, int EPW>
-__device__ __forceinline__ void load_seg_table(const V1Params* __restrict__ P, Scratch<N, EPW>& sh)
+__device__ __forceinline__ void load_seg_table(const V1Params& P, Scratch<N, EPW>& sh)
 {
     const int s = threadIdx.x;
     if (s < kNSeg) {
         SegLds g;
-        g.ax = P->sax[s];
-        g.ay = P->say[s];
-        g.sdx = P->sbx[s] - P->sax[s];
-        g.sdy = P->sby[s] - P->say[s];
-        g.L2 = P->L2[s];
-        g.rL2 = P->rL2[s];
+        g.ax = P.sax[s];
+        g.ay = P.say[s];
+        g.sdx = P.sbx[s] - P.sax[s];
+        g.sdy = P.sby[s] - P.say[s];
+        g.L2 = P.L2[s];
+        g.rL2 = P.rL2[s];
         sh.seg[s] = g;
     }
     __syncthreads();
@@ -622,7 +796,8 @@ __device__ __forceinline__ void load_seg_table(const V1Params* __restrict__ P, S
 
 // Futbol.reset (envs_v1/futbol_env.py:146-150): owner draw, formation, space.step(1e-4)
 template <int N, int EPW>
-__device__ __forceinline__ void do_reset(const V1Params* __restrict__ P, const Lane<N, EPW>& L, Env<N>& e
+__device__ __forceinline__ void do_reset(const V1Params& P, const V1Params* __restrict__ R, const Lane<N, EPW>& L,
+                                         Env<N>& e
 #ifdef FUTBOL_STAMPS
                                          , unsigned long long* st_stamps, unsigned long long& _stamp_prev
 #endif
@@ -630,7 +805,7 @@ __device__ __forceinline__ void do_reset(const V1Params* __restrict__ P, const L
 {
     const uint32_t ev = e.meta.event();
     e.meta.set_event(ev + 1);
-    Stream rs(P->seed, P->env_base + (uint32_t)L.env, ev, 0);
+    Stream rs(R->seed, R->env_base + (uint32_t)L.env, ev, 0);
     e.meta.set_owner((uint32_t)rs.choice(2));
     e.meta.set_steps(0);
     position_to_initial<N>(P, e);
@@ -690,32 +865,34 @@ __device__ __forceinline__ void pass_target(const Env<N>& e, Stream& rs, int ar,
 
 // ---------------------------------------------------------------------------
 // Futbol.step (envs_v1/futbol_env.py:427-483) + DummyVecEnv auto-reset
+// P: geometry / physics constants (a constexpr object in the default-field instance,
+// the context's device copy otherwise); R: the context's device params (runtime fields)
 template <int N, int EPW, typename OT>
-__global__ void __launch_bounds__(EPW) v1_step_kernel(const V1Params* __restrict__ P, V1Ptrs st,
-                                                     const uint8_t* __restrict__ actions, OT* __restrict__ obs,
-                                                     OT* __restrict__ reward, uint8_t* __restrict__ done_out,
-                                                     OT* __restrict__ term_obs)
+__device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* __restrict__ R, Scratch<N, EPW>& sh,
+                                             V1Ptrs st, const uint8_t* __restrict__ actions, OT* __restrict__ obs,
+                                             OT* __restrict__ reward, uint8_t* __restrict__ done_out,
+                                             OT* __restrict__ term_obs)
 {
     using S = V1Shape<N>;
     constexpr int BL = S::BALL;
-    __shared__ Scratch<N, EPW> sh;
     load_seg_table<N, EPW>(P, sh);
     const int env = blockIdx.x * EPW + threadIdx.x;
-    const int B = P->B;
+    const int B = R->B;
     if (env >= B) return;
     const Lane<N, EPW> L{&sh, st.spill, st.ckey, st.cjn, (int)threadIdx.x, env, B};
 #ifdef FUTBOL_STAMPS
     unsigned long long* st_stamps = st.stamps;
     unsigned long long _stamp_prev = __builtin_amdgcn_s_memtime();
+    const unsigned long long _wave_real0 = __builtin_amdgcn_s_memrealtime(), _wave_cyc0 = _stamp_prev;
 #endif
     Env<N> e;
     load_env<N>(st, env, B, e);
-    const double W = P->W, H = P->H;
+    const double W = P.W, H = P.H;
     FUTBOL_STAMP(0);
 
     const uint32_t ev = e.meta.event();
     e.meta.set_event(ev + 1);
-    Stream rs(P->seed, P->env_base + (uint32_t)env, ev, 0);
+    Stream rs(R->seed, R->env_base + (uint32_t)env, ev, 0);
 
     // actions: left team from HBM, right team = action_space.sample() (:306-307, :429)
     int arrow[2 * N], key[2 * N];
@@ -751,56 +928,46 @@ __global__ void __launch_bounds__(EPW) v1_step_kernel(const V1Params* __restrict
         touch[k] = cc_hit(e.px[BL], e.py[BL], kBallR, e.px[k], e.py[k], kPlayerR);
     });
 
-    // _process_action per player, then owner update (:309-422, :447-453)
+    // _process_action per player, then owner update (:309-422, :447-453).
+    // Shoot, press and pass all apply S * d / |d| for one direction d (shoot: goal - ball,
+    // S = 120; press: ball - player, S = 40; pass: teammate - ball, S = 100), so each
+    // player computes ONE sqrt and two divisions on the selected operands, and every
+    // branch outcome is applied with exact selects (no +-0 additions) -- identical
+    // results to the reference's five-way branch, without executing all of its arms.
     uint32_t owner = e.meta.owner();
     sfor<2 * N>([&](auto K) {
         constexpr int k = K;
         constexpr int side = k < N ? 0 : 1;
         const int ar = arrow[k], ky = key[k];
+        const bool tk = touch[k];
         const int fx = ar == 2 ? 1 : (ar == 4 ? -1 : 0);
         const int fy = ar == 1 ? 1 : (ar == 3 ? -1 : 0);
-        if (ky <= 1) {  // noop / dash: impulse 20 / 40, then _ball_move_with_player
-            const int f = ky == 0 ? 20 : 40;
-            e.vx[k] = e.vx[k] + (double)(f * fx) * kPlayerMinv;
-            e.vy[k] = e.vy[k] + (double)(f * fy) * kPlayerMinv;
-            if (touch[k]) {
-                e.vx[BL] = e.vx[k];
-                e.vy[BL] = e.vy[k];
-            }
-        } else if (ky == 2) {  // shoot
-            if (touch[k]) {
-                const double gx = side == 0 ? W : 0.0, gy = H / 2;
-                const double dx = gx - e.px[BL], dy = gy - e.py[BL];
-                const double mag = sqrt(dx * dx + dy * dy);
-                const double fbx = 120.0 * dx / mag, fby = 120.0 * dy / mag;
-                e.vx[BL] = e.vx[BL] / 2;
-                e.vy[BL] = e.vy[BL] / 2;
-                owner = side;
-                e.vx[BL] = e.vx[BL] + fbx * kBallMinv;
-                e.vy[BL] = e.vy[BL] + fby * kBallMinv;
-            }
-        } else if (ky == 3) {  // press: only without ball and without arrow
-            if (!touch[k] && ar == 0) {
-                const double dx = e.px[BL] - e.px[k], dy = e.py[BL] - e.py[k];
-                const double mag = sqrt(dx * dx + dy * dy);
-                e.vx[k] = e.vx[k] + (40.0 * dx / mag) * kPlayerMinv;
-                e.vy[k] = e.vy[k] + (40.0 * dy / mag) * kPlayerMinv;
-            }
-        } else {  // pass
-            if (touch[k]) {
-                double tx, ty;
-                pass_target<N, side, k - side * N>(e, rs, ar, tx, ty);
-                const double dx = tx - e.px[BL], dy = ty - e.py[BL];
-                const double mag = sqrt(dx * dx + dy * dy);
-                const double fbx = 100.0 * dx / mag, fby = 100.0 * dy / mag;
-                e.vx[BL] = e.vx[BL] / 10;
-                e.vy[BL] = e.vy[BL] / 10;
-                owner = side;
-                e.vx[BL] = e.vx[BL] + fbx * kBallMinv;
-                e.vy[BL] = e.vy[BL] + fby * kBallMinv;
-            }
-        }
-        if (touch[k]) owner = side;
+        const bool move = ky <= 1;                      // noop / dash (:331-341)
+        const bool shoot = ky == 2 && tk;               // (:344-368)
+        const bool press = ky == 3 && !tk && ar == 0;   // (:371-391)
+        const bool pass = ky == 4 && tk;                // (:394-419)
+        double tx = 0.0, ty = 0.0;
+        if (pass) pass_target<N, side, k - side * N>(e, rs, ar, tx, ty);
+        const double gx = side == 0 ? W : 0.0, gy = H / 2;
+        const double ox = press ? e.px[k] : e.px[BL], oy = press ? e.py[k] : e.py[BL];
+        const double qx = press ? e.px[BL] : (shoot ? gx : tx), qy = press ? e.py[BL] : (shoot ? gy : ty);
+        const double dx = qx - ox, dy = qy - oy;
+        const double mag = sqrt(dx * dx + dy * dy);
+        const double S = press ? 40.0 : (shoot ? 120.0 : 100.0);
+        const double fdx = S * dx / mag, fdy = S * dy / mag;
+        // player velocity: move impulse (f * arrow) / m, or the press impulse
+        const int f = ky == 0 ? 20 : 40;
+        const double mvx = e.vx[k] + (double)(f * fx) * kPlayerMinv, mvy = e.vy[k] + (double)(f * fy) * kPlayerMinv;
+        const double pvx = e.vx[k] + fdx * kPlayerMinv, pvy = e.vy[k] + fdy * kPlayerMinv;
+        e.vx[k] = move ? mvx : (press ? pvx : e.vx[k]);
+        e.vy[k] = move ? mvy : (press ? pvy : e.vy[k]);
+        // ball velocity: dribble (ball takes the player's velocity) or a kick (v/2 or v/10, + impulse)
+        const double D = shoot ? 2.0 : 10.0, rD = shoot ? 0.5 : 0.1;
+        const double kvx = cdiv(e.vx[BL], D, rD) + fdx * kBallMinv, kvy = cdiv(e.vy[BL], D, rD) + fdy * kBallMinv;
+        const bool dribble = move && tk, kick = shoot || pass;
+        e.vx[BL] = dribble ? e.vx[k] : (kick ? kvx : e.vx[BL]);
+        e.vy[BL] = dribble ? e.vy[k] : (kick ? kvy : e.vy[BL]);
+        owner = tk ? (uint32_t)side : owner;
     });
 
     // check_and_fix_out_bounds (:247-287), before physics
@@ -847,7 +1014,7 @@ __global__ void __launch_bounds__(EPW) v1_step_kernel(const V1Params* __restrict
 #pragma unroll 1
     for (int ph = 0; ph < 3; ++ph) {
         if (ph == 1 && !goal) continue;
-        if (ph == 2 && !(done && P->auto_reset)) continue;
+        if (ph == 2 && !(done && R->auto_reset)) continue;
         if (ph == 1) position_to_initial<N>(P, e);
         if (ph == 2) {
             if (term_obs) write_obs<N, OT>(e, term_obs + (size_t)env * (4 * S::Nb));
@@ -856,7 +1023,7 @@ __global__ void __launch_bounds__(EPW) v1_step_kernel(const V1Params* __restrict
             ret = 0.0;
             const uint32_t ev2 = e.meta.event();
             e.meta.set_event(ev2 + 1);
-            rs = Stream(P->seed, P->env_base + (uint32_t)env, ev2, 0);
+            rs = Stream(R->seed, R->env_base + (uint32_t)env, ev2, 0);
             e.meta.set_owner((uint32_t)rs.choice(2));
             e.meta.set_steps(0);
             position_to_initial<N>(P, e);
@@ -896,10 +1063,10 @@ __global__ void __launch_bounds__(EPW) v1_step_kernel(const V1Params* __restrict
             uint32_t steps = e.meta.steps() + 1;
             steps = steps > (uint32_t)kMaxSteps ? (uint32_t)kMaxSteps : steps;  // saturate (no auto-reset)
             e.meta.set_steps(steps);
-            done = (int)steps >= P->K_done;
+            done = (int)steps >= R->K_done;
             ret = st.ep_ret[env] + r;
-            if (done && !P->auto_reset) {
-                if ((int)steps == P->K_done) {
+            if (done && !R->auto_reset) {
+                if ((int)steps == R->K_done) {
                     st.stat_ret[env] = st.stat_ret[env] + ret;
                     st.stat_cnt[env] = st.stat_cnt[env] + 1;
                 }
@@ -916,19 +1083,51 @@ __global__ void __launch_bounds__(EPW) v1_step_kernel(const V1Params* __restrict
     done_out[env] = done ? 1 : 0;
     store_env<N>(st, env, B, e);
     FUTBOL_STAMP(10);
+#ifdef FUTBOL_STAMPS
+    // snapshot of THIS launch (overwritten every launch): start / end realtime (100 MHz),
+    // wave cycles, and where the wave ran (HW_ID: wave, simd, cu, sh, se | XCC_ID << 32)
+    if ((threadIdx.x & 63) == 0 && st_stamps) {
+        unsigned long long* w = &st_stamps[(size_t)(blockIdx.x * EPW / 64) * 16];
+        const unsigned long long real1 = __builtin_amdgcn_s_memrealtime();
+        const unsigned long long cyc1 = __builtin_amdgcn_s_memtime();
+        const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+        const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+        w[11] = _wave_real0;
+        w[12] = real1;
+        w[13] = cyc1 - _wave_cyc0;
+        w[14] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+    }
+#endif
+}
+
+// DEF: the registered ids' default field (v1_default_geometry<N>), constants as immediates
+template <int N, int EPW, typename OT, bool DEF>
+__global__ void __launch_bounds__(EPW) v1_step_kernel(const V1Params* __restrict__ R, V1Ptrs st,
+                                                      const uint8_t* __restrict__ actions, OT* __restrict__ obs,
+                                                      OT* __restrict__ reward, uint8_t* __restrict__ done_out,
+                                                      OT* __restrict__ term_obs)
+{
+    __shared__ Scratch<N, EPW> sh;
+    if constexpr (DEF) {
+        constexpr V1Params G = v1_default_geometry<N>();
+        v1_step_body<N, EPW, OT>(G, R, sh, st, actions, obs, reward, done_out, term_obs);
+    } else {
+        v1_step_body<N, EPW, OT>(*R, R, sh, st, actions, obs, reward, done_out, term_obs);
+    }
 }
 
 // futbol_create (init=1: Futbol.__init__, which ends in reset()) / futbol_reset (masked)
 template <int N, int EPW, typename OT>
-__global__ void __launch_bounds__(EPW) v1_reset_kernel(const V1Params* __restrict__ P, V1Ptrs st,
+__global__ void __launch_bounds__(EPW) v1_reset_kernel(const V1Params* __restrict__ R, V1Ptrs st,
                                                       const uint8_t* __restrict__ mask, OT* __restrict__ obs,
                                                       int init)
 {
     using S = V1Shape<N>;
+    const V1Params& P = *R;
     __shared__ Scratch<N, EPW> sh;
     load_seg_table<N, EPW>(P, sh);
     const int env = blockIdx.x * EPW + threadIdx.x;
-    const int B = P->B;
+    const int B = R->B;
     if (env >= B) return;
     if (mask && !mask[env]) return;
     const Lane<N, EPW> L{&sh, st.spill, st.ckey, st.cjn, (int)threadIdx.x, env, B};
@@ -936,8 +1135,8 @@ __global__ void __launch_bounds__(EPW) v1_reset_kernel(const V1Params* __restric
     if (init) {
         sfor<S::Nb>([&](auto K) {
             constexpr int k = K;
-            e.px[k] = P->fx[k];
-            e.py[k] = P->fy[k];
+            e.px[k] = P.fx[k];
+            e.py[k] = P.fy[k];
             e.vx[k] = e.vy[k] = e.bx[k] = e.by[k] = 0.0;
         });
         e.meta.w = 0;
@@ -951,7 +1150,7 @@ __global__ void __launch_bounds__(EPW) v1_reset_kernel(const V1Params* __restric
     unsigned long long* st_stamps = nullptr;
     unsigned long long _stamp_prev = 0;
 #endif
-    do_reset<N, EPW>(P, L, e
+    do_reset<N, EPW>(P, R, L, e
 #ifdef FUTBOL_STAMPS
                 , st_stamps, _stamp_prev
 #endif

@@ -1,7 +1,11 @@
+# envs-per-wave A/B on one box (FUTBOL_EPW selects the v1 kernel instantiation)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests/test_gpu_v1_parity.py -x -q > gpurun_out/pytest_epw32.log 2>&1 && \
-FUTBOL_EPW=16 timeout -k 10 600 python -m pytest tests/test_gpu_v1_parity.py -x -q -k "free_running or crowded" > gpurun_out/pytest_epw16.log 2>&1 && \
-for E in 64 32 16; do FUTBOL_EPW=$E timeout -k 10 120 python bench.py --steps 3000 --no-cpu-baseline > gpurun_out/bench_e$E.log 2>&1 || exit 1; done && \
-for E in 64 32 16; do FUTBOL_EPW=$E timeout -k 10 120 python bench.py --stamps --warmup 100 --steps 190 --profile-steps 10 > gpurun_out/stamps_e$E.log 2>&1 || exit 1; done
+OUT=gpurun_out/${AB_OUT:-epw}.log; : > $OUT
+for rep in 1 2; do
+  for e in ${EPWS:-64 32}; do
+    FUTBOL_EPW=$e timeout -k 10 200 python bench.py --no-cpu-baseline --steps 1500 ${BENCH_ARGS:-} > gpurun_out/ab_one.log 2>&1 || exit 1
+    echo "$e $(tail -1 gpurun_out/ab_one.log)" >> $OUT
+  done
+done

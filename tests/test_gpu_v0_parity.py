@@ -37,10 +37,14 @@ def test_free_running_bit_exact(random_opp):
         o2, r2, d2, term2 = ora.step(a.cpu().numpy().astype(np.int32).reshape(-1))
         o1, r1, d1 = obs.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy()
         assert np.array_equal(d1, d2), "done differs at %d" % t
-        assert np.array_equal(r1, r2), "reward differs at %d (max %g)" % (t, np.abs(r1 - r2).max())
-        assert np.array_equal(o1, o2), "obs differs at %d (max %g)" % (t, np.abs(o1 - o2).max())
+        # bitwise (also the sign of zero)
+        assert np.array_equal(r1.view(np.uint64), r2.view(np.uint64)), "reward differs at %d (max %g)" % (
+            t, np.abs(r1 - r2).max())
+        assert np.array_equal(o1.view(np.uint64), o2.view(np.uint64)), "obs differs at %d (max %g)" % (
+            t, np.abs(o1 - o2).max())
         if d1.any():
-            assert np.array_equal(info["terminal_observation"].cpu().numpy()[d1], term2[d1])
+            assert np.array_equal(info["terminal_observation"].cpu().numpy()[d1].view(np.uint64),
+                                  term2[d1].view(np.uint64))
         shots += int((o1[:, 4, 4] >= 4).sum())
     assert shots > 0
 

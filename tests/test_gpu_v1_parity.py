@@ -28,7 +28,8 @@ def _compare_state(venv, ora, n, B, tag):
     ob = v1_oracle_bodies(ora.envs, n, B)
     for f in ("px", "py", "vx", "vy", "bx", "by"):
         d = np.abs(st[f] - ob[f]).max()
-        assert np.array_equal(st[f], ob[f]), "%s: %s differs (max %g)" % (tag, f, d)
+        # bitwise: also the sign of zero
+        assert np.array_equal(st[f].view(np.uint64), ob[f].view(np.uint64)), "%s: %s differs (max %g)" % (tag, f, d)
     ex, age, jn = v1_dense_cache(st, n, B)
     ex2, age2, jn2 = v1_oracle_dense_cache(ora.envs, n, B)
     assert np.array_equal(ex, ex2), tag + ": arbiter cache membership"
@@ -58,10 +59,11 @@ def test_free_running_rollout_bit_exact(n, B, T):
         o2, r2, d2, term2 = ora.step(a_np)
         o1, r1, d1 = obs.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy()
         assert np.array_equal(d1, d2), "done differs at step %d" % t
-        assert np.array_equal(r1, r2), "reward differs at step %d: max %g" % (t, np.abs(r1 - r2).max())
-        assert np.array_equal(o1, o2), "obs differs at step %d: max %g" % (t, np.abs(o1 - o2).max())
+        assert np.array_equal(r1.view(np.uint64), r2.view(np.uint64)), "reward differs at step %d: max %g" % (t, np.abs(r1 - r2).max())
+        assert np.array_equal(o1.view(np.uint64), o2.view(np.uint64)), "obs differs at step %d: max %g" % (t, np.abs(o1 - o2).max())
         if d1.any():
-            assert np.array_equal(info["terminal_observation"].cpu().numpy()[d1], term2[d1])
+            assert np.array_equal(info["terminal_observation"].cpu().numpy()[d1].view(np.uint64),
+                                  term2[d1].view(np.uint64))
         goals += int((np.abs(r1) > 500).sum())
         dones += int(d1.sum())
         if t % 97 == 0:
@@ -164,3 +166,34 @@ def test_sharding_invariance():
         oh, rh, dh, _ = hi.step(a[B // 2:].contiguous())
         assert torch.equal(of, torch.cat([ol, oh])) and torch.equal(rf, torch.cat([rl, rh]))
         assert torch.equal(df, torch.cat([dl, dh]))
+
+
+def _rollout_equal(venv, ora, n, B, T, tag):
+    assert np.array_equal(venv.reset().cpu().numpy(), ora.reset())
+    for t in range(T):
+        a = venv.random_actions(t, seed=77)
+        obs, rew, done, info = venv.step(a)
+        o2, r2, d2, term2 = ora.step(a.cpu().numpy().astype(np.int32))
+        assert np.array_equal(done.cpu().numpy(), d2), (tag, t)
+        assert np.array_equal(rew.cpu().numpy().view(np.uint64), r2.view(np.uint64)), (tag, t)
+        assert np.array_equal(obs.cpu().numpy().view(np.uint64), o2.view(np.uint64)), (tag, t)
+    _compare_state(venv, ora, n, B, tag)
+
+
+@pytest.mark.parametrize("n", [2, 5])
+def test_generic_geometry_kernel(n, monkeypatch):
+    """The runtime-geometry instance (forced with FUTBOL_GENERIC=1) on the default field."""
+    monkeypatch.setenv("FUTBOL_GENERIC", "1")
+    B = 256
+    venv = _venv(n, B, seed=41)
+    _rollout_equal(venv, O.V1Vec(B, N=n, seed=41, portable=True), n, B, 320, "generic")
+    venv.close()
+
+
+def test_custom_field_size():
+    """A non-default width/height (Futbol(width=90, height=60)) selects the generic instance."""
+    from gym_futbol_amd import FutbolVecEnv
+    B, n = 256, 2
+    venv = FutbolVecEnv("v1", B, seed=3, dtype=torch.float64, number_of_player=n, width=90, height=60)
+    _rollout_equal(venv, O.V1Vec(B, N=n, seed=3, width=90.0, height=60.0, portable=True), n, B, 320, "90x60")
+    venv.close()
