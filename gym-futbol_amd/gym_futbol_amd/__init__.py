@@ -9,8 +9,11 @@ from .registration import ENV_SPECS, make, register_with_gym, spec
 from .vec_env import FutbolVecEnv, SB3VecEnv
 from .envs_v1 import Futbol
 from .envs import FutbolEnv
+from .evaluation import evaluate_policy
+from .policy import SB2MlpPolicy
 
 __all__ = ["make", "spec", "ENV_SPECS", "FutbolVecEnv", "SB3VecEnv", "Futbol", "FutbolEnv", "NativeError",
-           "LIB_PATH", "load_native"]
+           "LIB_PATH", "load_native",
+           "evaluate_policy", "SB2MlpPolicy"]
 
 register_with_gym()
