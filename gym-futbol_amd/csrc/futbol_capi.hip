@@ -43,7 +43,7 @@ struct FutbolCtx {
     size_t state_bytes = 0;
     std::vector<Field> fields;
     double* d_spill = nullptr;
-    unsigned long long* d_invalid = nullptr;  // [0] invalid-action count, [1] counter-driven fill launches x blocks
+    unsigned long long* d_invalid = nullptr;  // [0] invalid-action count, [1] / [2] counters of the counter-driven fills (blocks)
     V1Ptrs v1{};
     V0Ptrs v0{};
     double steps_since_clear = 0.0;
@@ -267,9 +267,9 @@ extern "C" int futbol_create(const FutbolConfig* cfg, int32_t device, uint64_t s
     };
     if ((he = hipMalloc((void**)&ctx->d_state, ctx->state_bytes)) != hipSuccess) return bail(he, "hipMalloc(state)");
     if ((he = hipMemset(ctx->d_state, 0, ctx->state_bytes)) != hipSuccess) return bail(he, "hipMemset(state)");
-    if ((he = hipMalloc((void**)&ctx->d_invalid, 2 * sizeof(unsigned long long))) != hipSuccess)
+    if ((he = hipMalloc((void**)&ctx->d_invalid, 3 * sizeof(unsigned long long))) != hipSuccess)
         return bail(he, "hipMalloc(counters)");
-    if ((he = hipMemset(ctx->d_invalid, 0, 2 * sizeof(unsigned long long))) != hipSuccess)
+    if ((he = hipMemset(ctx->d_invalid, 0, 3 * sizeof(unsigned long long))) != hipSuccess)
         return bail(he, "hipMemset");
 
     auto fptr = [&](const char* name) -> char* {
@@ -463,6 +463,20 @@ extern "C" int futbol_fill_actions(FutbolCtx* ctx, uint64_t seed, uint64_t step,
     if (launch_fill_actions(seed, step, ctr, (uint32_t)ctx->env_base, ctx->B, ctx->act_dim, nvals, actions,
                             (hipStream_t)stream))
         return fail(ctx, FUTBOL_EHIP, "fill_actions launch failed");
+    return FUTBOL_OK;
+}
+
+extern "C" int futbol_fill_actions_steps(FutbolCtx* ctx, uint64_t seed, uint64_t step, int32_t nsteps,
+                                         uint8_t* actions, void* stream)
+{
+    if (!ctx || !actions || nsteps <= 0 || nsteps > 65535) return FUTBOL_EINVAL;
+    FB_CHECK_HIP(ctx, hipSetDevice(ctx->device));
+    int nvals = 5;
+    if (ctx->cfg.env_kind == FUTBOL_ENV_V0) nvals = ctx->cfg.action_as_int0 ? 16 : 4;
+    unsigned long long* ctr = step == ~(uint64_t)0 ? ctx->d_invalid + 2 : nullptr;
+    if (launch_fill_actions_steps(seed, step, nsteps, ctr, (uint32_t)ctx->env_base, ctx->B, ctx->act_dim, nvals,
+                                  actions, (hipStream_t)stream))
+        return fail(ctx, FUTBOL_EHIP, "fill_actions_steps launch failed");
     return FUTBOL_OK;
 }
 

@@ -85,6 +85,8 @@ int launch_v0(const V0Params* P, int B, const V0Ptrs& st, int out64, int what, c
 
 int launch_fill_actions(uint64_t seed, uint64_t step, unsigned long long* step_ctr, uint32_t env_base, int B,
                         int adim, int nvals, uint8_t* actions, hipStream_t stream);
+int launch_fill_actions_steps(uint64_t seed, uint64_t step0, int nsteps, unsigned long long* ctr, uint32_t env_base,
+                              int B, int adim, int nvals, uint8_t* actions, hipStream_t stream);
 int launch_episode_stats(const double* stat_ret, const uint32_t* stat_cnt, int B, double steps, double* out3,
                          int clear, double* stat_ret_w, uint32_t* stat_cnt_w, hipStream_t stream);
 

@@ -6,7 +6,21 @@
 
 namespace futbol {
 
-// actions[i][j] = floor(U * nvals), U = draw j of (seed, env_base + i, event = step, tag 1):
+// Synthetic-policy actions of one env-step: action j = (w * nvals) >> 32 with w = word j % 4 of
+// Philox block j / 4 of (seed, env, event = step, tag 1) -- four actions per block.
+__device__ __forceinline__ void synthetic_actions(uint64_t seed, uint32_t env_id, uint32_t step, int adim, int nvals,
+                                                  uint8_t* out)
+{
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    for (int b = 0; b * 4 < adim; ++b) {
+        const Philox4 p = philox4x32_10((uint32_t)b, step, env_id, 1u, k0, k1);
+        for (int q = 0; q < 4 && b * 4 + q < adim; ++q)
+            out[b * 4 + q] = (uint8_t)(((unsigned long long)p.x[q] * (unsigned)nvals) >> 32);
+    }
+}
+
+
+// actions[i] = synthetic_actions(seed, env_base + i, step):
 // the benchmark's "left agent" (random_action() for the left team, envs_v1/futbol_env.py:306-307).
 // fill_ctr != nullptr: the step is this launch's index among the context's counter-driven fills
 // (0, 1, 2, ...): every block adds 1 to the counter and divides the old value by the grid size,
@@ -25,14 +39,40 @@ __global__ void __launch_bounds__(256) fill_actions_kernel(uint64_t seed, uint32
     const int env = blockIdx.x * blockDim.x + threadIdx.x;
     if (env >= B) return;
     const uint32_t s = fill_ctr ? s_step : step;
-    Stream rs(seed, env_base + (uint32_t)env, s, 1);
-    for (int j = 0; j < adim; ++j) actions[(size_t)env * adim + j] = (uint8_t)rs.choice(nvals);
+    synthetic_actions(seed, env_base + (uint32_t)env, s, adim, nvals, actions + (size_t)env * adim);
 }
 int launch_fill_actions(uint64_t seed, uint64_t step, unsigned long long* step_ctr, uint32_t env_base, int B,
                         int adim, int nvals, uint8_t* actions, hipStream_t stream)
 {
     hipLaunchKernelGGL(fill_actions_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, seed, (uint32_t)step,
                        step_ctr, env_base, B, adim, nvals, actions);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// actions[t][i][j] for t < nsteps: the fills of steps step0 .. step0 + nsteps - 1 in one launch
+// (grid.y = nsteps).  fill_ctr != nullptr: step0 = *fill_ctr, a step counter that
+// advance_counter_kernel moves on by nsteps right after, in stream order (one plain load per
+// thread here; a per-block atomic would serialise tens of thousands of same-address atomics).
+__global__ void __launch_bounds__(256) fill_actions_steps_kernel(uint64_t seed, uint32_t step0,
+                                                                 const unsigned long long* fill_ctr,
+                                                                 uint32_t env_base, int B, int adim, int nvals,
+                                                                 uint8_t* __restrict__ actions)
+{
+    const int env = blockIdx.x * blockDim.x + threadIdx.x;
+    if (env >= B) return;
+    const uint32_t t = blockIdx.y;
+    const uint32_t s = (fill_ctr ? (uint32_t)*fill_ctr : step0) + t;
+    synthetic_actions(seed, env_base + (uint32_t)env, s, adim, nvals, actions + ((size_t)t * B + env) * adim);
+}
+
+__global__ void advance_counter_kernel(unsigned long long* ctr, unsigned long long by) { *ctr += by; }
+
+int launch_fill_actions_steps(uint64_t seed, uint64_t step0, int nsteps, unsigned long long* ctr, uint32_t env_base,
+                              int B, int adim, int nvals, uint8_t* actions, hipStream_t stream)
+{
+    hipLaunchKernelGGL(fill_actions_steps_kernel, dim3((B + 255) / 256, nsteps), dim3(256), 0, stream, seed,
+                       (uint32_t)step0, ctr, env_base, B, adim, nvals, actions);
+    if (ctr) hipLaunchKernelGGL(advance_counter_kernel, dim3(1), dim3(1), 0, stream, ctr, (unsigned long long)nsteps);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

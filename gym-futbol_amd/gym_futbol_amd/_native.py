@@ -45,6 +45,8 @@ SIGNATURES = [
     ("futbol_step", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                               C.c_void_p]),
     ("futbol_fill_actions", C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p]),
+    ("futbol_fill_actions_steps", C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_int32, C.c_void_p,
+                                             C.c_void_p]),
     ("futbol_episode_stats", C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]),
     ("futbol_invalid_actions", C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_void_p]),
     ("futbol_state_bytes", C.c_int, [C.c_void_p, C.POINTER(C.c_size_t)]),

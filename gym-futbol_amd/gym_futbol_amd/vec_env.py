@@ -133,6 +133,15 @@ class FutbolVecEnv:
                                                      _stream_ptr(self.device)), self.ctx.h)
         return out
 
+    def random_actions_steps(self, nsteps, step, seed=1234, out=None):
+        """Synthetic actions of `nsteps` consecutive steps in one launch: [nsteps, B, action_dim]."""
+        if out is None:
+            out = torch.empty((nsteps, self.num_envs, self.action_dim), dtype=torch.uint8, device=self.device)
+        with torch.cuda.device(self.device):
+            nat.check(nat.load().futbol_fill_actions_steps(self.ctx.h, int(seed), int(step), int(nsteps),
+                                                           out.data_ptr(), _stream_ptr(self.device)), self.ctx.h)
+        return out
+
     def episode_stats(self, clear=False):
         """Device f64[3] = [sum of finished-episode returns, #episodes, #env-steps] since last clear."""
         with torch.cuda.device(self.device):

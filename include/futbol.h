@@ -96,13 +96,22 @@ int futbol_reset(FutbolCtx* ctx, const uint8_t* mask, void* obs, void* stream);
 int futbol_step(FutbolCtx* ctx, const uint8_t* actions, void* obs, void* reward, uint8_t* done,
                 void* terminal_obs, void* stream);
 
-/* Synthetic policy: actions[i] = iid uniform action of env (env_id_base+i) at
-   `step` from the tag-1 Philox stream keyed by `seed`.  step == UINT64_MAX: the
+/* Synthetic policy: actions[i] = iid uniform actions of env (env_id_base+i) at
+   `step`: action j = (w * nvals) >> 32, w = word j % 4 of the Philox4x32-10 block
+   (counter {j / 4, step, env id, 1}, key = seed).  step == UINT64_MAX: the
    step is the number of earlier UINT64_MAX calls on this context (0, 1, 2, ...),
    counted on the device, so a captured hipGraph draws fresh actions per replay.
    The counter is independent of futbol_step: a fill may run on another stream
    concurrently with a step (double-buffered actions). */
 int futbol_fill_actions(FutbolCtx* ctx, uint64_t seed, uint64_t step, uint8_t* actions, void* stream);
+
+/* The fills of `nsteps` consecutive steps in one launch: actions [nsteps][B][action_dim],
+   slice t = futbol_fill_actions(ctx, seed, step + t, ...).  step == UINT64_MAX: step is
+   the total nsteps of the earlier UINT64_MAX calls of this function on the context (a
+   device counter of its own, advanced in stream order).  For benchmark loops: the synthetic policy does not depend on
+   observations, so a graph of K steps can draw all K steps' actions up front. */
+int futbol_fill_actions_steps(FutbolCtx* ctx, uint64_t seed, uint64_t step, int32_t nsteps, uint8_t* actions,
+                              void* stream);
 
 /* Episode statistics since the last clear: out3 (device, f64[3]) =
    {sum of finished-episode returns, finished episodes, env-steps}. */

@@ -13,6 +13,7 @@
  *     event  per-env counter, +1 for every step() and every reset()
  *     env_id global env id (shard invariant)
  *     tag    0 = env stream, 1 = synthetic benchmark/left-agent actions
+ *            (4 actions per block: action j = (word j%4 of block j/4) * n >> 32)
  *
  * Conversions (fixed, identical everywhere):
  *   U        = ((x0>>5)*2^26 + (x1>>6)) / 2^53               in [0,1)

@@ -112,7 +112,7 @@ class Tape:
 
 
 def synthetic_action(seed, env_id, step, j, n):
-    """Synthetic 'left agent' action stream (tag 1): floor(U * n)."""
-    t = Tape(seed, env_id, step, tag=1)
-    t.j = j
-    return t.choice_index(n)
+    """Synthetic 'left agent' (benchmark policy) action j of an env-step (tag 1): four actions
+    per Philox block, action j = (w * n) >> 32 with w = word j % 4 of block j // 4."""
+    x = philox4x32_10((j // 4, step & MASK, env_id & MASK, 1), (seed & MASK, (seed >> 32) & MASK))
+    return (x[j % 4] * n) >> 32

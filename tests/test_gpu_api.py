@@ -211,6 +211,13 @@ def test_random_actions_follow_the_tape(kind, kw, nvals):
         exp = np.array([[synthetic_action(99, base + i, step, j, nvals) for j in range(venv.action_dim)]
                         for i in range(B)])
         assert np.array_equal(a, exp)
+    many = venv.random_actions_steps(5, 40, seed=99).cpu().numpy()    # steps 40..44 in one launch
+    for t in range(5):
+        assert np.array_equal(many[t], venv.random_actions(40 + t, seed=99).cpu().numpy())
+    c0 = venv.random_actions_steps(3, 2**64 - 1, seed=99).cpu().numpy()   # counter-driven: steps 0..2
+    c1 = venv.random_actions_steps(3, 2**64 - 1, seed=99).cpu().numpy()   # then 3..5
+    assert np.array_equal(c0, venv.random_actions_steps(3, 0, seed=99).cpu().numpy())
+    assert np.array_equal(c1, venv.random_actions_steps(3, 3, seed=99).cpu().numpy())
     for k in range(3):   # counter-driven fills: the k-th such call draws step k
         a = venv.random_actions(2**64 - 1, seed=99).cpu().numpy()
         assert np.array_equal(a, venv.random_actions(k, seed=99, out=torch.empty_like(venv._act)).cpu().numpy())
