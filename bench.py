@@ -147,6 +147,9 @@ def main():
     ap.add_argument("--players", type=int, default=2)
     ap.add_argument("--kind", default="v1", choices=["v1", "v0"])
     ap.add_argument("--graph", type=int, default=1, help="replay the timed steps from a hipGraph")
+    ap.add_argument("--groups", type=int, default=1,
+                    help="step the B envs as this many independent env groups (B/groups envs each: one "
+                         "context, HIP stream and hipGraph per group) that advance asynchronously")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=600,
                     help="steps timed per-kernel with HIP events (a multiple of the episode length)")
@@ -215,43 +218,88 @@ def main():
     # timed loop: hipGraph of G steps.  The synthetic policy does not look at observations,
     # so one launch draws the actions of all G steps ([G, B, 2N] u8 in HBM, fresh at every
     # replay) and each step kernel reads its slice -- instead of G small fill launches.
-    graph = None
+    # --groups g > 1: the B envs of this GPU are stepped as g independent groups of B/g envs
+    # (their own contexts with env ids base + k*B/g.., so every env's trajectory is the same
+    # as in the one-context run), each on its own HIP stream replaying its own graph.  A
+    # group's next step waits only for ITS previous step, so the waves of one group's step
+    # fill the SIMDs that another group's slowest waves leave idle (EnvPool-style async
+    # groups; the per-launch roofline above is measured on the single full-batch launch).
+    ngroups = max(1, int(args.groups))
+    if B % ngroups or (B // ngroups) % 64:
+        raise SystemExit("--groups must split --envs into multiples of 64")
+    if ngroups > 1:
+        kw_g = dict(kw)
+        groups = [FutbolVecEnv(args.kind, B // ngroups, device=dev, seed=0,
+                               env_id_base=R.shard(B) + g * (B // ngroups), dtype=torch.float32, **kw_g)
+                  for g in range(ngroups)]
+        for ge in groups:
+            ge.reset()
+    else:
+        groups = [venv]
+    streams = [torch.cuda.Stream(dev) for _ in groups]
+
+    graphs = None
     G = 100
     if args.graph:
-        abuf = torch.empty((G,) + tuple(act.shape), dtype=torch.uint8, device=dev)
-        graph = torch.cuda.CUDAGraph()
-        s = torch.cuda.Stream(dev)
-        s.wait_stream(stream)
-        with torch.cuda.stream(s):
-            with torch.cuda.graph(graph, stream=s):
-                venv.random_actions_steps(G, ALL, seed=1234, out=abuf)
-                for t in range(G):
-                    venv.step_raw(abuf[t])
-        stream.wait_stream(s)
+        graphs = []
+        for ge, s in zip(groups, streams):
+            abuf = torch.empty((G, ge.num_envs, ge.action_dim), dtype=torch.uint8, device=dev)
+            if ge is not venv:  # warm the group up like the main context
+                for _ in range(args.warmup):
+                    ge.random_actions(ALL, seed=1234, out=ge._act)
+                    ge.step_raw(ge._act)
+            g_ = torch.cuda.CUDAGraph()
+            s.wait_stream(stream)
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g_, stream=s):
+                    ge.random_actions_steps(G, ALL, seed=1234, out=abuf)
+                    for t in range(G):
+                        ge.step_raw(abuf[t])
+            stream.wait_stream(s)
+            graphs.append((g_, abuf))
         torch.cuda.synchronize(dev)
+    elif ngroups > 1:
+        raise SystemExit("--groups needs --graph 1")
+
+    def all_stats():
+        tot = torch.zeros(3, dtype=torch.float64, device=dev)
+        for ge in groups:
+            tot += ge.episode_stats(clear=False)
+        return tot
 
     stats_buf = torch.zeros(3, dtype=torch.float64, device=dev)
-    venv.episode_stats(clear=True)
+    for ge in groups:
+        ge.episode_stats(clear=True)
     D.barrier(dev)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     done_steps = 0
     while done_steps < args.steps:
-        chunk = min(G, args.steps - done_steps) if graph is not None else 1
-        if graph is not None and chunk == G:
-            graph.replay()
+        chunk = min(G, args.steps - done_steps) if graphs is not None else 1
+        if graphs is not None and chunk == G:
+            for (g_, _), s in zip(graphs, streams):
+                with torch.cuda.stream(s):
+                    g_.replay()
+        elif ngroups > 1:
+            for ge, s in zip(groups, streams):
+                with torch.cuda.stream(s):
+                    for _ in range(chunk):
+                        ge.random_actions(ALL, seed=1234, out=ge._act)
+                        ge.step_raw(ge._act)
         else:
             for _ in range(chunk):
                 one_step()
         prev = done_steps
         done_steps += chunk
         if R.distributed and done_steps // 300 != prev // 300:
-            stats_buf.copy_(venv.episode_stats(clear=False))
+            for s in streams:
+                stream.wait_stream(s)
+            stats_buf.copy_(all_stats())
             D.reduce_episode_stats(stats_buf)  # RCCL over xGMI: [sum return, episodes, env-steps]
     torch.cuda.synchronize(dev)
     D.barrier(dev)
     elapsed = D.max_over_ranks(time.perf_counter() - t0, dev)
-    stats = D.reduce_episode_stats(venv.episode_stats(clear=False).clone()).cpu().numpy()
+    stats = D.reduce_episode_stats(all_stats().clone()).cpu().numpy()
 
     total_env_steps = B * args.steps * world
     value = total_env_steps / elapsed
@@ -267,7 +315,7 @@ def main():
                                 % (B, n, n)) if args.kind == "v1" else
                    ("C3: %d envs/GPU v0 FutbolEnv, hard-coded opponent" % B),
                    "envs_per_gpu": B, "global_envs": B * world, "parallelism": "dp%d" % world,
-                   "obs_dtype": "f32", "hip_graph": bool(graph is not None)},
+                   "obs_dtype": "f32", "hip_graph": bool(graphs is not None), "env_groups": ngroups},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "v1_step_kernel<%d,float>" % n if args.kind == "v1" else "v0_step_kernel<float>",
@@ -283,6 +331,9 @@ def main():
         line["cpu_baseline"] = cpu_baseline(args.kind, n)
     if rank == 0:
         print(json.dumps(line), flush=True)
+    for ge in groups:
+        if ge is not venv:
+            ge.close()
     venv.close()
     D.shutdown()
 

@@ -403,8 +403,27 @@ __device__ __forceinline__ bool far_from_segments(double x, double y, double rea
 
 // ---------------------------------------------------------------------------
 // cpSpaceStep(dt) for one env.  dtc: 1 -> 1e-4, 2 -> 0.1
+// the first CK arbiter-cache entries (ck = pair | age << 12, 0xffff = none; cj = jnAcc), loaded
+// unconditionally (c < CK <= P is always in bounds) so that the loads carry no dependence on
+// ncache and can be issued together with the body state at the top of the kernel
 template <int N, int EPW>
-__device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>& L, Env<N>& e, int dtc
+__device__ __forceinline__ void load_cache_pre(const Lane<N, EPW>& L, uint32_t ncache, uint32_t (&ck)[CK],
+                                               double (&cj)[CK])
+{
+    static_assert(CK <= V1Shape<N>::P, "preloaded cache entries must lie inside the [P][B] arrays");
+#pragma unroll
+    for (int c = 0; c < CK; ++c) {
+        const uint32_t k = L.ckey[(size_t)c * L.B + L.env];
+        const double j = L.cjn[(size_t)c * L.B + L.env];
+        ck[c] = (uint32_t)c < ncache ? k : 0xffffu;
+        cj[c] = (uint32_t)c < ncache ? j : 0.0;
+    }
+}
+
+// ck / cj: the preloaded cache entries (load_cache_pre) of the env's CURRENT cache
+template <int N, int EPW>
+__device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>& L, Env<N>& e, int dtc,
+                                           const uint32_t (&ck)[CK], const double (&cj)[CK]
 #ifdef FUTBOL_STAMPS
                                            , unsigned long long* st_stamps, unsigned long long& _stamp_prev
 #endif
@@ -422,18 +441,6 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
     const int B = L.B, env = L.env;
     const uint32_t ncache = e.meta.ncache();
 
-    // arbiter cache: first CK entries into registers, with independent loads
-    uint32_t ck[CK];
-    double cj[CK];
-#pragma unroll
-    for (int c = 0; c < CK; ++c) {
-        ck[c] = 0xffffu;
-        cj[c] = 0.0;
-        if ((uint32_t)c < ncache) {
-            ck[c] = L.ckey[(size_t)c * B + env];
-            cj[c] = L.cjn[(size_t)c * B + env];
-        }
-    }
     uint32_t touched = 0;  // preloaded entries matched by this step's contacts
 
     // cpBodyUpdatePosition
@@ -809,7 +816,10 @@ __device__ __forceinline__ void do_reset(const V1Params& P, const V1Params* __re
     e.meta.set_owner((uint32_t)rs.choice(2));
     e.meta.set_steps(0);
     position_to_initial<N>(P, e);
-    space_step<N, EPW>(P, L, e, 1
+    uint32_t ck[CK];
+    double cj[CK];
+    load_cache_pre<N, EPW>(L, e.meta.ncache(), ck, cj);
+    space_step<N, EPW>(P, L, e, 1, ck, cj
 #ifdef FUTBOL_STAMPS
                   , st_stamps, _stamp_prev
 #endif
@@ -875,18 +885,48 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
 {
     using S = V1Shape<N>;
     constexpr int BL = S::BALL;
-    load_seg_table<N, EPW>(P, sh);
-    const int env = blockIdx.x * EPW + threadIdx.x;
     const int B = R->B;
-    if (env >= B) return;
+    // lanes past B (last block) shadow env B-1's loads, which are in bounds, and return
+    // after the segment table's barrier without storing anything
+    const int env_raw = blockIdx.x * EPW + threadIdx.x;
+    const bool live = env_raw < B;
+    const int env = live ? env_raw : B - 1;
     const Lane<N, EPW> L{&sh, st.spill, st.ckey, st.cjn, (int)threadIdx.x, env, B};
 #ifdef FUTBOL_STAMPS
     unsigned long long* st_stamps = st.stamps;
     unsigned long long _stamp_prev = __builtin_amdgcn_s_memtime();
     const unsigned long long _wave_real0 = __builtin_amdgcn_s_memrealtime(), _wave_cyc0 = _stamp_prev;
 #endif
+    // every HBM read of the step is issued here, in one batch, before the segment table's
+    // barrier: the body state, the first CK arbiter-cache entries and the running return
+    // (one memory round trip per step)
     Env<N> e;
     load_env<N>(st, env, B, e);
+    uint32_t ck[CK];
+    double cj[CK];
+    load_cache_pre<N, EPW>(L, e.meta.ncache(), ck, cj);
+    const double ep_ret0 = st.ep_ret[env];
+    // the left team's actions: 2N bytes per env, as 32-bit words when 2N % 4 == 0 (rows stay
+    // 4-byte aligned), 16-bit words otherwise
+    uint32_t araw[2 * N];
+    if constexpr ((2 * N) % 4 == 0) {
+        const uint32_t* a32 = (const uint32_t*)(actions + (size_t)env * (2 * N));
+        sfor<(2 * N) / 4>([&](auto W4) {
+            constexpr int w = W4;
+            const uint32_t x = a32[w];
+            sfor<4>([&](auto Q) { araw[4 * w + Q] = (x >> (8 * Q)) & 0xffu; });
+        });
+    } else {
+        const uint16_t* a16 = (const uint16_t*)(actions + (size_t)env * (2 * N));
+        sfor<N>([&](auto W2) {
+            constexpr int w = W2;
+            const uint32_t x = a16[w];
+            araw[2 * w] = x & 0xffu;
+            araw[2 * w + 1] = x >> 8;
+        });
+    }
+    load_seg_table<N, EPW>(P, sh);
+    if (!live) return;
     const double W = P.W, H = P.H;
     FUTBOL_STAMP(0);
 
@@ -899,7 +939,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
     int bad = 0;
     sfor<2 * N>([&](auto I) {
         constexpr int i = I;
-        int a = actions[(size_t)env * (2 * N) + i];
+        int a = (int)araw[i];
         bad += a > 4;
         a = a > 4 ? 4 : a;
         if constexpr (i & 1) key[i >> 1] = a; else arrow[i >> 1] = a;
@@ -1029,7 +1069,8 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
             position_to_initial<N>(P, e);
         }
         FUTBOL_STAMP(ph == 0 ? 3 : 9);
-        space_step<N, EPW>(P, L, e, ph == 0 ? 2 : 1
+        if (ph != 0) load_cache_pre<N, EPW>(L, e.meta.ncache(), ck, cj);  // the cache phase 0 left behind
+        space_step<N, EPW>(P, L, e, ph == 0 ? 2 : 1, ck, cj
 #ifdef FUTBOL_STAMPS
                       , st_stamps, _stamp_prev
 #endif
@@ -1064,7 +1105,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
             steps = steps > (uint32_t)kMaxSteps ? (uint32_t)kMaxSteps : steps;  // saturate (no auto-reset)
             e.meta.set_steps(steps);
             done = (int)steps >= R->K_done;
-            ret = st.ep_ret[env] + r;
+            ret = ep_ret0 + r;
             if (done && !R->auto_reset) {
                 if ((int)steps == R->K_done) {
                     st.stat_ret[env] = st.stat_ret[env] + ret;
