@@ -11,9 +11,11 @@ from .envs_v1 import Futbol
 from .envs import FutbolEnv
 from .evaluation import evaluate_policy
 from .policy import SB2MlpPolicy
+from .ppo import PPO2, ActorCritic
+from .monitor import VecMonitor, EvalCallback, load_results
 
 __all__ = ["make", "spec", "ENV_SPECS", "FutbolVecEnv", "SB3VecEnv", "Futbol", "FutbolEnv", "NativeError",
            "LIB_PATH", "load_native",
-           "evaluate_policy", "SB2MlpPolicy"]
+           "evaluate_policy", "SB2MlpPolicy", "PPO2", "ActorCritic", "VecMonitor", "EvalCallback", "load_results"]
 
 register_with_gym()
