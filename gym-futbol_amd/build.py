@@ -28,6 +28,10 @@ CFLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-ffp-contract=off", "-
           "-Wall", "-Wno-unused-function", "-I" + os.path.join(ROOT, "include")]
 if VARIANT == "stamps":
     CFLAGS.append("-DFUTBOL_STAMPS")
+if VARIANT == "crumbs":  # diagnostic: per-wave phase markers in host-coherent memory
+    CFLAGS.append("-DFUTBOL_CRUMBS")
+if VARIANT == "bounds":  # diagnostic: index checks that flag and clamp instead of faulting
+    CFLAGS.append("-DFUTBOL_BOUNDS")
 
 
 def _deps():

@@ -316,6 +316,13 @@ extern "C" int futbol_create(const FutbolConfig* cfg, int32_t device, uint64_t s
             return bail(he, "hipMemset(stamps)");
         s.stamps = ctx->d_stamps;
 #endif
+#ifdef FUTBOL_CRUMBS
+        if ((he = hipHostMalloc((void**)&ctx->d_stamps, (size_t)((B + 63) / 64 + 1) * 16 * 8,
+                                hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
+            return bail(he, "hipHostMalloc(crumbs)");
+        memset(ctx->d_stamps, 0, (size_t)((B + 63) / 64 + 1) * 16 * 8);
+        s.stamps = ctx->d_stamps;
+#endif
         int rc = launch_v1(N, ctx->epw, ctx->v1_def, (const V1Params*)ctx->d_params, B, s, 0, 1, nullptr, nullptr, nullptr,
                            nullptr, nullptr, nullptr, 1, 0);
         if (rc) return bail(hipGetLastError(), "launch(init)");
@@ -351,7 +358,11 @@ extern "C" int futbol_destroy(FutbolCtx* ctx)
     if (ctx->d_spill) hipFree(ctx->d_spill);
     if (ctx->d_params) hipFree(ctx->d_params);
     if (ctx->d_invalid) hipFree(ctx->d_invalid);
+#ifdef FUTBOL_CRUMBS
+    if (ctx->d_stamps) hipHostFree(ctx->d_stamps);
+#else
     if (ctx->d_stamps) hipFree(ctx->d_stamps);
+#endif
     for (auto e : ctx->t_ev)
         if (e) hipEventDestroy(e);
     delete ctx;
@@ -550,6 +561,11 @@ extern "C" int futbol_debug_stamps(FutbolCtx* ctx, uint64_t* host_out, int64_t n
     if (!ctx->d_stamps) return fail(ctx, FUTBOL_EUNSUPPORTED, "not a FUTBOL_STAMPS diagnostic build / not v1");
     const size_t bytes = (size_t)((ctx->B + 63) / 64) * 16 * 8;
     if ((size_t)n * 8 < bytes) return fail(ctx, FUTBOL_EINVAL, "stamps buffer too small");
+#ifdef FUTBOL_CRUMBS
+    memcpy(host_out, ctx->d_stamps, bytes);  // host memory: readable even after a device fault
+    (void)clear;
+    return FUTBOL_OK;
+#endif
     FB_CHECK_HIP(ctx, hipSetDevice(ctx->device));
     FB_CHECK_HIP(ctx, hipDeviceSynchronize());
     FB_CHECK_HIP(ctx, hipMemcpy(host_out, ctx->d_stamps, bytes, hipMemcpyDeviceToHost));

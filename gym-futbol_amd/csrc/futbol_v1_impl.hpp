@@ -61,6 +61,34 @@ constexpr int CK = 4;       // arbiter-cache entries preloaded into registers
 #define FUTBOL_STAMP(slot) do { } while (0)
 #endif
 
+// Diagnostic builds only.
+// -DFUTBOL_BOUNDS (FUTBOL_BUILD_VARIANT=bounds): index checks that set bit 40 + code of the
+// invalid-action counter and clamp the index instead of faulting.
+// -DFUTBOL_CRUMBS (FUTBOL_BUILD_VARIANT=crumbs): every wave publishes the last phase it entered
+// into host-coherent memory (system scope), readable after a device fault.
+#ifdef FUTBOL_BOUNDS
+#define FB_BOUND(L, cond, code, fix)                                                                     \
+    do {                                                                                                  \
+        if (!(cond)) {                                                                                    \
+            atomicOr((L).dbg, 1ull << (40 + (code)));                                                     \
+            fix;                                                                                          \
+        }                                                                                                 \
+    } while (0)
+#else
+#define FB_BOUND(L, cond, code, fix) do { } while (0)
+#endif
+#ifdef FUTBOL_CRUMBS
+#define FUTBOL_CRUMB(L, k)                                                                                \
+    do {                                                                                                  \
+        if (((L).lane & 63) == 0)                                                                         \
+            __hip_atomic_store(&(L).crumbs[(size_t)blockIdx.x * 16], (unsigned long long)(k),            \
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);                              \
+        __threadfence_system();                                                                           \
+    } while (0)
+#else
+#define FUTBOL_CRUMB(L, k) do { } while (0)
+#endif
+
 template <int N>
 struct V1Shape {
     static constexpr int Nb = 2 * N + 1;
@@ -141,8 +169,19 @@ struct Lane {
     uint16_t* ckey;
     double* cjn;
     int lane, env, B;
+#ifdef FUTBOL_BOUNDS
+    unsigned long long* dbg;
+#endif
+#ifdef FUTBOL_CRUMBS
+    unsigned long long* crumbs;
+#endif
 
-    __device__ __forceinline__ double* sp(int s, int f) const { return spill + ((size_t)(s - KL) * 8 + f) * B + env; }
+    __device__ __forceinline__ double* sp(int s, int f) const
+    {
+        int t = s - KL;
+        FB_BOUND(*this, t >= 0 && t < S::P - KL, 0, t = 0);
+        return spill + ((size_t)t * 8 + f) * B + env;
+    }
     // record s as 4 double2 (any slot)
     __device__ __forceinline__ double2 get(int s, int q) const
     {
@@ -439,7 +478,8 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
     const double slop = P.slop, W = P.W, H = P.H;
     e.meta.set_dtcode(dtc);
     const int B = L.B, env = L.env;
-    const uint32_t ncache = e.meta.ncache();
+    uint32_t ncache = e.meta.ncache();
+    FB_BOUND(L, ncache <= (uint32_t)S::P, 1, ncache = S::P);
 
     uint32_t touched = 0;  // preloaded entries matched by this step's contacts
 
@@ -452,6 +492,7 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
         e.by[k] = 0.0;
     });
 
+    FUTBOL_CRUMB(L, 10 + dtc);
     // collide in canonical order; cpArbiterUpdate + preStep folded in (needs pre-damping v)
     int n = 0;
     auto record = [&](int a, int bcode, int pair, double nx, double ny, double p1x, double p1y, double p2x,
@@ -475,6 +516,7 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
                 normal = (ck[c] >> 12) == 0;  // touched by the previous step: NORMAL -> warm start
                 touched |= 1u << c;
             }
+        FB_BOUND(L, n < S::P && pair < S::P, 5, n = S::P - 1);
         L.set_rec(n, nx, ny, nMass, bias, bounce, jn, pack_info(a, bcode, pair, normal));
         ++n;
     };
@@ -530,6 +572,7 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
         });
     });
 
+    FUTBOL_CRUMB(L, 40 + dtc);
     FUTBOL_STAMP(dtc == 2 ? 4 : 9);
     // cache entries beyond the preloaded ones (rare): look them up in global memory
     if (ncache > (uint32_t)CK) {
@@ -684,6 +727,7 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
         }
     }
 
+    FUTBOL_CRUMB(L, 60 + dtc);
     FUTBOL_STAMP(dtc == 2 ? 6 : 9);
     // cpSpaceArbiterSetFilter + store jnAcc: survivors (untouched, age+1 < 3) then this step's contacts
     uint32_t w = 0;
@@ -692,7 +736,9 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
         if ((uint32_t)c < ncache) {
             const uint32_t key = ck[c], age = key >> 12;
             if (!((touched >> c) & 1u) && age + 1 < 3) {
+                FB_BOUND(L, w < (uint32_t)S::P, 6, w = S::P - 1);
                 L.ckey[(size_t)w * B + env] = (uint16_t)((key & 0x3ffu) | ((age + 1) << 12));
+                FB_BOUND(L, w < (uint32_t)S::P, 6, w = S::P - 1);
                 L.cjn[(size_t)w * B + env] = cj[c];
                 ++w;
             }
@@ -705,17 +751,23 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
         bool t = false;
         for (int s = 0; s < n; ++s) t |= ((L.get_info(s) >> 11) & 511) == pair;
         if (!t && age + 1 < 3) {
+            FB_BOUND(L, w < (uint32_t)S::P, 6, w = S::P - 1);
             L.cjn[(size_t)w * B + env] = L.cjn[(size_t)c * B + env];
+            FB_BOUND(L, w < (uint32_t)S::P, 6, w = S::P - 1);
             L.ckey[(size_t)w * B + env] = (uint16_t)(pair | ((age + 1) << 12));
             ++w;
         }
     }
     for (int s = 0; s < n; ++s) {
+        FB_BOUND(L, w < (uint32_t)S::P, 6, w = S::P - 1);
         L.ckey[(size_t)w * B + env] = (uint16_t)((L.get_info(s) >> 11) & 511);
+        FB_BOUND(L, w < (uint32_t)S::P, 6, w = S::P - 1);
         L.cjn[(size_t)w * B + env] = L.get_jn(s);
         ++w;
     }
+    FB_BOUND(L, w <= (uint32_t)S::P, 2, w = S::P);
     e.meta.set_ncache(w);
+    FUTBOL_CRUMB(L, 70 + dtc);
     FUTBOL_STAMP(dtc == 2 ? 7 : 9);
 }
 
@@ -891,7 +943,14 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
     const int env_raw = blockIdx.x * EPW + threadIdx.x;
     const bool live = env_raw < B;
     const int env = live ? env_raw : B - 1;
-    const Lane<N, EPW> L{&sh, st.spill, st.ckey, st.cjn, (int)threadIdx.x, env, B};
+    const Lane<N, EPW> L{&sh, st.spill, st.ckey, st.cjn, (int)threadIdx.x, env, B
+#ifdef FUTBOL_BOUNDS
+                         , st.invalid
+#endif
+#ifdef FUTBOL_CRUMBS
+                         , st.stamps
+#endif
+    };
 #ifdef FUTBOL_STAMPS
     unsigned long long* st_stamps = st.stamps;
     unsigned long long _stamp_prev = __builtin_amdgcn_s_memtime();
@@ -928,6 +987,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
     load_seg_table<N, EPW>(P, sh);
     if (!live) return;
     const double W = P.W, H = P.H;
+    FUTBOL_CRUMB(L, 1);
     FUTBOL_STAMP(0);
 
     const uint32_t ev = e.meta.event();
@@ -1043,6 +1103,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
         }
     }
     e.meta.set_owner(owner);
+    FUTBOL_CRUMB(L, 3);
     FUTBOL_STAMP(2);
 
     // Up to three cpSpaceSteps per call, through ONE inlined call site:
@@ -1118,11 +1179,13 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
         }
         FUTBOL_STAMP(ph == 0 ? 8 : 9);
     }
+    FUTBOL_CRUMB(L, 80);
     write_obs<N, OT>(e, obs + (size_t)env * (4 * S::Nb));
     st.ep_ret[env] = ret;
     reward[env] = (OT)r;
     done_out[env] = done ? 1 : 0;
     store_env<N>(st, env, B, e);
+    FUTBOL_CRUMB(L, 99);
     FUTBOL_STAMP(10);
 #ifdef FUTBOL_STAMPS
     // snapshot of THIS launch (overwritten every launch): start / end realtime (100 MHz),
@@ -1171,7 +1234,14 @@ __global__ void __launch_bounds__(EPW) v1_reset_kernel(const V1Params* __restric
     const int B = R->B;
     if (env >= B) return;
     if (mask && !mask[env]) return;
-    const Lane<N, EPW> L{&sh, st.spill, st.ckey, st.cjn, (int)threadIdx.x, env, B};
+    const Lane<N, EPW> L{&sh, st.spill, st.ckey, st.cjn, (int)threadIdx.x, env, B
+#ifdef FUTBOL_BOUNDS
+                         , st.invalid
+#endif
+#ifdef FUTBOL_CRUMBS
+                         , st.stamps
+#endif
+    };
     Env<N> e;
     if (init) {
         sfor<S::Nb>([&](auto K) {
