@@ -12,10 +12,11 @@ from .envs import FutbolEnv
 from .evaluation import evaluate_policy
 from .policy import SB2MlpPolicy
 from .ppo import PPO2, ActorCritic
+from .a2c import A2C
 from .monitor import VecMonitor, EvalCallback, load_results
 
 __all__ = ["make", "spec", "ENV_SPECS", "FutbolVecEnv", "SB3VecEnv", "Futbol", "FutbolEnv", "NativeError",
            "LIB_PATH", "load_native",
-           "evaluate_policy", "SB2MlpPolicy", "PPO2", "ActorCritic", "VecMonitor", "EvalCallback", "load_results"]
+           "evaluate_policy", "SB2MlpPolicy", "PPO2", "A2C", "ActorCritic", "VecMonitor", "EvalCallback", "load_results"]
 
 register_with_gym()

@@ -37,3 +37,18 @@ def test_ppo2_trains_on_gpu_env(tmp_path):
     assert (z["ep_lengths"] == 300).all()
     pol = gf.PPO2.load_policy(os.path.join(str(tmp_path), "best_model.pt"), eval_env.device)
     assert isinstance(pol, gf.ActorCritic)
+
+
+def test_a2c_runs_on_gpu_env():
+    """A2C (SB2 defaults: n_steps 5, RMSProp) on 4096 GPU envs: mechanics and finite losses."""
+    import gym_futbol_amd as gf
+    env = gf.make("Futbol2v2-v1", num_envs=4096, seed=4)
+    model = gf.A2C("CustomPolicy", env, seed=0)
+    model.learn(4096 * 5 * 120, log_interval=30)
+    assert model.num_timesteps == 4096 * 5 * 120
+    assert all(np.isfinite([r["policy_loss"], r["value_loss"], r["policy_entropy"]]).all() for r in model.logs)
+    assert any(r["ep_reward_mean"] is not None for r in model.logs)   # 600 steps: two episodes ended
+    obs = env.reset()
+    a, _ = model.predict(obs, deterministic=True)
+    assert a.shape == (4096, 4) and a.dtype == torch.int64 and int(a.max()) <= 4
+    env.close()

@@ -1,4 +1,4 @@
-"""PPO2 and Monitor / EvalCallback (§8(f) #4) on the CPU, driven by a small
+"""PPO2 and A2C and Monitor / EvalCallback (§8(f) #4) on the CPU, driven by a small
 torch env with the FutbolVecEnv surface (the GPU env itself is exercised in test_gpu_train.py).
 
 * GAE against a plain-Python restatement of stable-baselines 2's PPO2 Runner loop;
@@ -154,3 +154,51 @@ def test_eval_callback_writes_sb2_evaluations(tmp_path):
     assert z["timesteps"].tolist() == [32 * 16, 32 * 32, 32 * 48] and (z["ep_lengths"] == 10).all()
     assert os.path.exists(tmp_path / "best_model.pt")
     assert isinstance(PPO2.load_policy(str(tmp_path / "best_model.pt")), ActorCritic)
+
+
+def test_a2c_returns_match_sb2_discount_with_dones():
+    from gym_futbol_amd.a2c import discounted_returns
+    rng = np.random.default_rng(3)
+    T, B, gamma = 5, 6, 0.99
+    rew = rng.normal(size=(T, B))
+    dones = (rng.random((T, B)) < 0.3).astype(np.float64)
+    last = rng.normal(size=B)
+
+    def discount_with_dones(rewards, dones_, g):  # stable-baselines a2c/utils.py, as published
+        discounted, r = [], 0
+        for reward, done in zip(rewards[::-1], dones_[::-1]):
+            r = reward + g * r * (1.0 - done)
+            discounted.append(r)
+        return discounted[::-1]
+
+    exp = np.zeros((T, B))
+    for n in range(B):
+        r, d = list(rew[:, n]), list(dones[:, n])
+        if d[-1] == 0:
+            exp[:, n] = discount_with_dones(r + [last[n]], d + [0], gamma)[:-1]
+        else:
+            exp[:, n] = discount_with_dones(r, d, gamma)
+    got = discounted_returns(*(torch.as_tensor(x) for x in (rew, dones, last)), gamma)
+    assert np.allclose(got.numpy(), exp, rtol=1e-12, atol=1e-12)
+
+
+def test_tf_rmsprop_update():
+    from gym_futbol_amd.a2c import TFRMSProp
+    p = torch.nn.Parameter(torch.tensor([1.0, -2.0], dtype=torch.float64))
+    opt = TFRMSProp([p], lr=0.1, alpha=0.9, eps=1e-5)
+    p.grad = torch.tensor([0.5, 2.0], dtype=torch.float64)
+    opt.step()
+    ms = 0.9 * 1.0 + 0.1 * np.array([0.25, 4.0])        # TF1 initialises the slot to ones
+    assert np.allclose(p.detach().numpy(), np.array([1.0, -2.0]) - 0.1 * np.array([0.5, 2.0]) / np.sqrt(ms + 1e-5))
+
+
+def test_a2c_learns_contextual_bandit():
+    from gym_futbol_amd import A2C
+    env = BanditEnv(B=64, ep_len=10)
+    model = A2C([dict(pi=[32], vf=[32])], env, learning_rate=5e-3, ent_coef=0.0, seed=0)
+    model.learn(total_timesteps=64 * 5 * 1200, log_interval=200)
+    obs = env.reset()
+    a, _ = model.predict(obs, deterministic=True)
+    assert (a[:, 0] == obs[:, :5].argmax(1)).float().mean() > 0.9
+    # SB2's RMSProp slot starts at 1 (small first steps), so A2C needs ~1000 updates here
+    assert model.logs[-1]["ep_reward_mean"] > 6.5 > 3.0 > model.logs[1]["ep_reward_mean"]
