@@ -26,6 +26,8 @@ ARCH = os.environ.get("FUTBOL_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fPIC",
           "-Wall", "-Wno-unused-function", "-I" + os.path.join(ROOT, "include")]
+# A/B of compiler options: FUTBOL_EXTRA_CFLAGS="..." (with a FUTBOL_BUILD_VARIANT name)
+CFLAGS += os.environ.get("FUTBOL_EXTRA_CFLAGS", "").split()
 if VARIANT == "stamps":
     CFLAGS.append("-DFUTBOL_STAMPS")
 if VARIANT == "crumbs":  # diagnostic: per-wave phase markers in host-coherent memory
