@@ -50,13 +50,17 @@ def init(backend=None, use_gpu=True):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if use_gpu:
-        torch.cuda.set_device(local)
-        device = torch.device("cuda", local)
+        # rehearsal of the multi-rank path on a one-GPU box: FUTBOL_SHARE_DEVICE=1 puts every
+        # local rank on device local_rank % device_count (with FUTBOL_DIST_BACKEND=gloo, since RCCL
+        # refuses two ranks on one GPU)
+        dev_idx = local % max(1, torch.cuda.device_count()) if os.environ.get("FUTBOL_SHARE_DEVICE") else local
+        torch.cuda.set_device(dev_idx)
+        device = torch.device("cuda", dev_idx)
     else:
         device = torch.device("cpu")
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = backend or ("nccl" if use_gpu else "gloo")
+        backend = backend or os.environ.get("FUTBOL_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
         if backend == "nccl":
             dist.init_process_group(backend, device_id=device)
         else:
@@ -82,7 +86,7 @@ def max_over_ranks(seconds, device):
 
 def barrier(device):
     if dist.is_initialized() and dist.get_world_size() > 1:
-        if device.type == "cuda":
+        if device.type == "cuda" and dist.get_backend() == "nccl":
             dist.barrier(device_ids=[device.index])
         else:
             dist.barrier()
