@@ -515,19 +515,17 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
 
     FUTBOL_CRUMB(L, 10 + dtc);
     // bodies' positions (v_bias rows) and velocities (v rows) staged in LDS for the per-lane
-    // dynamic body index of the circle-pair contacts; the solver prologue overwrites both
+    // dynamic body index of the contact loops; the solver prologue overwrites both
     // (5v5: +6% step throughput; 2v2: -3% -- the staging and the bit loops cost more than the
     // 10 pair branches they replace, so few-body instances keep the branches)
     constexpr bool kCompactPairs = N >= 5;
     Scratch<N, EPW>* const sh_ = L.sh;
     const int ln_ = L.lane;
-    if constexpr (kCompactPairs) {
-        sfor<S::Nb>([&](auto K) {
-            constexpr int k = K;
-            sh_->vb[k][ln_] = make_double2(e.px[k], e.py[k]);
-            sh_->v[k][ln_] = make_double2(e.vx[k], e.vy[k]);
-        });
-    }
+    sfor<S::Nb>([&](auto K) {
+        constexpr int k = K;
+        sh_->vb[k][ln_] = make_double2(e.px[k], e.py[k]);
+        sh_->v[k][ln_] = make_double2(e.vx[k], e.vy[k]);
+    });
     // collide in canonical order; cpArbiterUpdate + preStep folded in (needs pre-damping v)
     int n = 0;
     auto record = [&](int a, int bcode, int pair, double nx, double ny, double p1x, double p1y, double p2x,
@@ -556,43 +554,66 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
         ++n;
     };
 
-    sfor<S::Nb>([&](auto I) {
-        constexpr int i = I;
-        constexpr double ri = i == S::BALL ? kBallR : kPlayerR;
-        constexpr double mi = i == S::BALL ? kBallMinv : kPlayerMinv;
-        const double cl = e.px[i] - ri, cb = e.py[i] - ri, cr = e.px[i] + ri, ct = e.py[i] + ri;
-        // every segment's cpBB lies within 1 of the field border: exact reject of all 12
-        const bool interior = cl > 1.0 && cr < W - 1.0 && cb > 1.0 && ct < H - 1.0;
-        if (!interior) {
-            // cpBBIntersects(circle, segment s) for all 12 segments from the 16 distinct bounds
+    // (1) circle-segment contacts of all bodies, (body, segment) ascending: cpBBIntersects from
+    // the 16 distinct segment bounds as a 12-bit field per body in 60-bit words (5 bodies per
+    // word); one contact test per set bit, so a wave runs max-over-lanes(candidates of the word)
+    // iterations rather than one loop per body that any lane needs.  The body is indexed
+    // dynamically through the LDS rows staged above.
+    constexpr int BPW = 5;
+    constexpr int NWS = (S::Nb + BPW - 1) / BPW;
+    sfor<NWS>([&](auto WD) {
+        constexpr int w = WD;
+        constexpr int i0 = w * BPW, i1 = (w + 1) * BPW < S::Nb ? (w + 1) * BPW : S::Nb;
+        uint64_t cand = 0;
+        sfor<i0, i1>([&](auto I) {
+            constexpr int i = I;
+            constexpr double ri = i == S::BALL ? kBallR : kPlayerR;
+            const double cl = e.px[i] - ri, cb = e.py[i] - ri, cr = e.px[i] + ri, ct = e.py[i] + ri;
+            // every segment's cpBB lies within 1 of the field border: exact reject of all 12
+            const bool interior = cl > 1.0 && cr < W - 1.0 && cb > 1.0 && ct < H - 1.0;
             const BBT& T = P.bbt;
             const bool r1 = cl <= T.r1, rW1 = cl <= T.rW1, rm1 = cl <= T.rm1, rW3 = cl <= T.rW3;
             const bool lm1 = T.lm1 <= cr, lW1 = T.lW1 <= cr, lm3 = T.lm3 <= cr, lWp1 = T.lWp1 <= cr;
             const bool tlo = cb <= T.tlo, tH = cb <= T.tH, t1 = cb <= T.t1, thi = cb <= T.thi;
             const bool bm1 = T.bm1 <= ct, bhi = T.bhi <= ct, bH = T.bH <= ct, blo = T.blo <= ct;
-            uint32_t cand = 0;
-            cand |= (r1 && lm1 && tlo && bm1) ? 1u << 0 : 0u;
-            cand |= (r1 && lm1 && tH && bhi) ? 1u << 1 : 0u;
-            cand |= (rW1 && lm1 && tH && bH) ? 1u << 2 : 0u;
-            cand |= (rW1 && lW1 && tlo && bm1) ? 1u << 3 : 0u;
-            cand |= (rW1 && lW1 && tH && bhi) ? 1u << 4 : 0u;
-            cand |= (rW1 && lm1 && t1 && bm1) ? 1u << 5 : 0u;
-            cand |= (rm1 && lm3 && thi && blo) ? 1u << 6 : 0u;
-            cand |= (r1 && lm3 && tlo && blo) ? 1u << 7 : 0u;
-            cand |= (r1 && lm3 && thi && bhi) ? 1u << 8 : 0u;
-            cand |= (rW3 && lWp1 && thi && blo) ? 1u << 9 : 0u;
-            cand |= (rW3 && lW1 && tlo && blo) ? 1u << 10 : 0u;
-            cand |= (rW3 && lW1 && thi && bhi) ? 1u << 11 : 0u;
-            while (cand) {  // ascending segment order, per-lane trip count
-                const int s = __builtin_ctz(cand);
-                cand &= cand - 1;
-                const SegLds g = L.sh->seg[s];
-                double nx, ny, p1x, p1y, p2x, p2y;
-                if (cs_test(e.px[i], e.py[i], ri, g, nx, ny, p1x, p1y, p2x, p2y))
-                    record(i, 32 + s, i * kNSeg + s, nx, ny, p1x, p1y, p2x, p2y, e.px[i], e.py[i], e.vx[i], e.vy[i],
-                           mi, 0.0, 0.0, 0.0, 0.0, 0.0, kE * 0.0);
-            }
+            uint32_t c = 0;
+            c |= (r1 && lm1 && tlo && bm1) ? 1u << 0 : 0u;
+            c |= (r1 && lm1 && tH && bhi) ? 1u << 1 : 0u;
+            c |= (rW1 && lm1 && tH && bH) ? 1u << 2 : 0u;
+            c |= (rW1 && lW1 && tlo && bm1) ? 1u << 3 : 0u;
+            c |= (rW1 && lW1 && tH && bhi) ? 1u << 4 : 0u;
+            c |= (rW1 && lm1 && t1 && bm1) ? 1u << 5 : 0u;
+            c |= (rm1 && lm3 && thi && blo) ? 1u << 6 : 0u;
+            c |= (r1 && lm3 && tlo && blo) ? 1u << 7 : 0u;
+            c |= (r1 && lm3 && thi && bhi) ? 1u << 8 : 0u;
+            c |= (rW3 && lWp1 && thi && blo) ? 1u << 9 : 0u;
+            c |= (rW3 && lW1 && tlo && blo) ? 1u << 10 : 0u;
+            c |= (rW3 && lW1 && thi && bhi) ? 1u << 11 : 0u;
+            cand |= interior ? 0ull : (uint64_t)c << (kNSeg * (i - i0));
+        });
+        while (cand) {
+            const int bit = __builtin_ctzll(cand);
+            cand &= cand - 1;
+            const int bi = bit / kNSeg;
+            const int sg = bit - bi * kNSeg;
+            const int i = i0 + bi;
+            const double2 pi_ = sh_->vb[i][ln_], vi = sh_->v[i][ln_];
+            const bool ball = i == S::BALL;
+            const double ri = ball ? kBallR : kPlayerR, mi = ball ? kBallMinv : kPlayerMinv;
+            const SegLds g = sh_->seg[sg];
+            double nx, ny, p1x, p1y, p2x, p2y;
+            if (cs_test(pi_.x, pi_.y, ri, g, nx, ny, p1x, p1y, p2x, p2y))
+                record(i, 32 + sg, i * kNSeg + sg, nx, ny, p1x, p1y, p2x, p2y, pi_.x, pi_.y, vi.x, vi.y, mi, 0.0,
+                       0.0, 0.0, 0.0, 0.0, kE * 0.0);
         }
+    });
+
+    // (2) circle-circle contacts, pairs (i, j > i) in row-major order
+    sfor<S::Nb>([&](auto I) {
+        constexpr int i = I;
+        constexpr double ri = i == S::BALL ? kBallR : kPlayerR;
+        constexpr double mi = i == S::BALL ? kBallMinv : kPlayerMinv;
+        const double cl = e.px[i] - ri, cb = e.py[i] - ri, cr = e.px[i] + ri, ct = e.py[i] + ri;
         if constexpr (!kCompactPairs) {
             // few bodies: one branch per pair (i, j > i), compile-time j
             sfor<i + 1, S::Nb>([&](auto J) {

@@ -12,8 +12,9 @@
  * with its deliberate simplifications:
  *   - angular DOFs dropped (A.6): the only torques come from contact lever arms
  *     that are collinear with the normal up to rounding (~1e-16 of the impulse);
- *   - canonical arbiter order (D.1): for body i ascending, its segments 0..11,
- *     then circle pairs (i, j>i).  Chipmunk's BBTree order is not reproducible.
+ *   - canonical arbiter order (D.1): every circle-segment pair (body i ascending,
+ *     segments 0..11), then every circle pair (i, j>i) row-major.  Chipmunk's
+ *     BBTree order is not reproducible.
  * Pinned instead by the hand-derived KATs in tests/test_oracle_v1.py.
  *
  * This file is deliberately written as "one env, plain structs, dense arbiter
@@ -223,7 +224,8 @@ void orc_v1_space_step(OrcV1 *e, double dt)
         e->bx[k] = 0.0; e->by[k] = 0.0;
     }
 
-    /* collide, canonical order */
+    /* collide, canonical order: all circle-segment pairs (body i ascending, segment
+     * ascending), then all circle-circle pairs (i < j, row-major) */
     for (int i = 0; i < Nb; ++i) {
         double ri = body_radius(e, i);
         double cl = e->px[i] - ri, cb = e->py[i] - ri, cr = e->px[i] + ri, ct = e->py[i] + ri;
@@ -237,6 +239,10 @@ void orc_v1_space_step(OrcV1 *e, double dt)
             if (circle_segment(e->px[i], e->py[i], ri, ax, ay, bx, by, SEG_RADIUS, &nx, &ny, &p1x, &p1y, &p2x, &p2y))
                 collide_pair(e, list, &n, i, -1 - s, i * ORC_NSEG + s, nx, ny, p1x, p1y, p2x, p2y);
         }
+    }
+    for (int i = 0; i < Nb; ++i) {
+        double ri = body_radius(e, i);
+        double cl = e->px[i] - ri, cb = e->py[i] - ri, cr = e->px[i] + ri, ct = e->py[i] + ri;
         for (int j = i + 1; j < Nb; ++j) {
             double rj = body_radius(e, j);
             if (!bb_intersects(cl, cb, cr, ct, e->px[j] - rj, e->py[j] - rj, e->px[j] + rj, e->py[j] + rj)) continue;
