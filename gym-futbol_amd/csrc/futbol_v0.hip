@@ -28,6 +28,7 @@ constexpr int kViewsLive = 6, kRowValid = 7;
 
 struct Env {
     double r[5][5];
+    double vw[8];  // frozen Easy_Agent views (x, y) x 4, loaded with the state
     uint32_t owner, last_owner;
     bool views_live;
     bool pending_done;
@@ -58,12 +59,6 @@ struct Ctx {
     Stream* rs;
 };
 
-__device__ __forceinline__ void load_view(const Ctx& c, int a, double& x, double& y)
-{
-    x = c.view[(size_t)(2 * a) * c.B + c.env];
-    y = c.view[(size_t)(2 * a + 1) * c.B + c.env];
-}
-
 // defence_near (:280-289) with the agent's (possibly stale) Easy_Agent view
 template <int a>
 __device__ __forceinline__ int defence_near(const Ctx& c, const Env& e)
@@ -74,7 +69,8 @@ __device__ __forceinline__ int defence_near(const Ctx& c, const Env& e)
         vx = e.r[a][0];
         vy = e.r[a][1];
     } else {
-        load_view(c, a, vx, vy);
+        vx = e.vw[2 * a];
+        vy = e.vw[2 * a + 1];
     }
     constexpr int o = a < 2 ? 2 : 0;
     double t0, t1;
@@ -321,6 +317,8 @@ __device__ __forceinline__ void rebind(const Ctx& c, Env& e)
         e.views_live = false;
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
+            e.vw[2 * a] = e.r[a][0];
+            e.vw[2 * a + 1] = e.r[a][1];
             c.view[(size_t)(2 * a) * c.B + c.env] = e.r[a][0];
             c.view[(size_t)(2 * a + 1) * c.B + c.env] = e.r[a][1];
         }
@@ -345,6 +343,10 @@ __device__ __forceinline__ void load(const V0Ptrs& st, int env, int B, Env& e, M
     for (int r = 0; r < 5; ++r)
 #pragma unroll
         for (int f = 0; f < 5; ++f) e.r[r][f] = st.row[(size_t)(r * 5 + f) * B + env];
+    // the views with the rows, in the same batch of loads: read on every step once the views are
+    // frozen (after the first goal or reset), and then the only other HBM reads of the step
+#pragma unroll
+    for (int k = 0; k < 8; ++k) e.vw[k] = st.view[(size_t)k * B + env];
     m.w = st.meta[env];
     e.owner = m.owner();
     e.last_owner = m.last_owner();
@@ -382,6 +384,7 @@ __global__ void __launch_bounds__(64) v0_step_kernel(const V0Params* __restrict_
     Env e;
     Meta m;
     load(st, env, B, e, m);
+    const double ep_ret0 = st.ep_ret[env];
     const bool row_valid_before = m.bit(kRowValid);
     const uint32_t ev = m.event();
     m.set_event(ev + 1);
@@ -461,7 +464,7 @@ __global__ void __launch_bounds__(64) v0_step_kernel(const V0Params* __restrict_
     if ((int)steps + 1 >= P->K_done) done = true;  // time >= game_time, checked before time += 0.1
     m.set_steps(steps + 1 > (uint32_t)kMaxSteps ? (uint32_t)kMaxSteps : steps + 1);
 
-    double ret = st.ep_ret[env] + rw;
+    double ret = ep_ret0 + rw;
     bool row_valid = true;
     if (done && !P->auto_reset) {
         st.stat_ret[env] = st.stat_ret[env] + ret;
