@@ -12,8 +12,9 @@
 // reference's operation order everywhere, so results are bit-identical to the
 // CPU oracle (tests/test_gpu_v1_parity.py).  Division by a constant c uses
 // q0 = x*rc, r = fma(-q0, c, x), q = fma(r, rc, q0) with rc = RN(1/c)
-// (Markstein's correction: correctly rounded, verified on 5.2e8 samples per
-// divisor, tests/test_gpu_numerics.py).
+// (Markstein's correction; equal to the IEEE quotient for every constant divisor the
+// default-geometry kernels use on 6e6 random and near-midpoint samples each,
+// tests/test_cdiv.py).
 //
 // Contacts: narrowphase over all Nb*12 circle-segment and Nb(Nb-1)/2
 // circle-circle pairs in the canonical order with exact
