@@ -7,7 +7,7 @@
 // tag 0 = env stream, tag 1 = synthetic left-agent actions (benchmark policy).
 // Draw conversions: SURVEY.md Appendix C.  Because the counter carries the
 // GLOBAL env id, an env's trajectory does not depend on how envs are sharded
-// over GPUs (tests/test_sharding.py).
+// over GPUs (tests/test_distributed_gloo.py, tests/test_gpu_v1_parity.py::test_sharding_invariance).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
