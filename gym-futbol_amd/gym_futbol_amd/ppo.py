@@ -156,6 +156,31 @@ def gae_returns(rewards, values, dones, last_values, last_dones, gamma, lam):
     return adv + values
 
 
+def ppo_loss(policy, obs, actions, returns, values, neglogp_old, clip, clip_vf, ent_coef, vf_coef):
+    """SB2 PPO2's minibatch loss (ppo2.py `setup_model` / `_train_step`): advantages normalised
+    over the minibatch, clipped surrogate, clipped value loss (clip_vf None: no clipping here --
+    PPO2.learn passes the policy's clip range, as SB2 does), entropy bonus.  Returns the loss
+    and the detached [pg_loss, vf_loss, entropy, approxkl, clipfrac]."""
+    adv = returns - values
+    adv = (adv - adv.mean()) / (adv.std(unbiased=False) + 1e-8)
+    logits, v = policy(obs)
+    nlp, ent = policy.neglogp_entropy(logits, actions)
+    entropy = ent.mean()
+    if clip_vf is None:
+        vf_loss = 0.5 * ((v - returns) ** 2).mean()
+    else:
+        v_clip = values + torch.clamp(v - values, -clip_vf, clip_vf)
+        vf_loss = 0.5 * torch.maximum((v - returns) ** 2, (v_clip - returns) ** 2).mean()
+    ratio = torch.exp(neglogp_old - nlp)
+    pg_loss = torch.maximum(-adv * ratio, -adv * torch.clamp(ratio, 1.0 - clip, 1.0 + clip)).mean()
+    loss = pg_loss - entropy * ent_coef + vf_loss * vf_coef
+    with torch.no_grad():
+        approxkl = 0.5 * ((nlp - neglogp_old) ** 2).mean()
+        clipfrac = ((ratio - 1.0).abs() > clip).float().mean()
+        parts = torch.stack([pg_loss.detach(), vf_loss.detach(), entropy.detach(), approxkl, clipfrac])
+    return loss, parts
+
+
 class PPO2:
     """PPO2(policy, env, ...) with SB2's constructor arguments and learn()/predict()/save()/load().
 
@@ -259,29 +284,13 @@ class PPO2:
             perm = torch.randperm(self.n_batch, device=self.device, generator=self.generator)
             for s in range(0, self.n_batch, mb):
                 idx = perm[s:s + mb]
-                R, V0, NLP0 = returns[idx], values[idx], neglogp_old[idx]
-                adv = R - V0
-                adv = (adv - adv.mean()) / (adv.std(unbiased=False) + 1e-8)
-                logits, v = self.policy(obs[idx])
-                nlp, ent = self.policy.neglogp_entropy(logits, actions[idx])
-                entropy = ent.mean()
-                if clip_vf is None:
-                    vf_loss = 0.5 * ((v - R) ** 2).mean()
-                else:
-                    v_clip = V0 + torch.clamp(v - V0, -clip_vf, clip_vf)
-                    vf_loss = 0.5 * torch.maximum((v - R) ** 2, (v_clip - R) ** 2).mean()
-                ratio = torch.exp(NLP0 - nlp)
-                pg_loss = torch.maximum(-adv * ratio, -adv * torch.clamp(ratio, 1.0 - clip, 1.0 + clip)).mean()
-                loss = pg_loss - entropy * self.ent_coef + vf_loss * self.vf_coef
+                loss, parts = ppo_loss(self.policy, obs[idx], actions[idx], returns[idx], values[idx],
+                                       neglogp_old[idx], clip, clip_vf, self.ent_coef, self.vf_coef)
                 self.optimizer.zero_grad(set_to_none=True)
                 loss.backward()
                 torch.nn.utils.clip_grad_norm_(self.policy.parameters(), self.max_grad_norm)
                 self.optimizer.step()
-                with torch.no_grad():
-                    approxkl = 0.5 * ((nlp - NLP0) ** 2).mean()
-                    clipfrac = ((ratio - 1.0).abs() > clip).float().mean()
-                    stats.append(torch.stack([pg_loss.detach(), vf_loss.detach(), entropy.detach(), approxkl,
-                                              clipfrac]))
+                stats.append(parts)
         return torch.stack(stats).mean(0)
 
     def learn(self, total_timesteps, callback=None, log_interval=1, reset_num_timesteps=True):

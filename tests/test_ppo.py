@@ -1,7 +1,8 @@
 """PPO2 and A2C and Monitor / EvalCallback (§8(f) #4) on the CPU, driven by a small
 torch env with the FutbolVecEnv surface (the GPU env itself is exercised in test_gpu_train.py).
 
-* GAE against a plain-Python restatement of stable-baselines 2's PPO2 Runner loop;
+* GAE against a plain-Python restatement of stable-baselines 2's PPO2 Runner loop, and the
+  minibatch loss (clipped surrogate, clipped value loss, entropy, approxkl, clipfrac) against numpy;
 * learning: PPO2 solves a contextual bandit (reward 1 for picking the arg-max observation);
 * save / load round trip (torch.load weights_only=True);
 * VecMonitor CSV (SB2 Monitor format) and EvalCallback's evaluations.npz (the keys, dtypes and
@@ -202,3 +203,42 @@ def test_a2c_learns_contextual_bandit():
     assert (a[:, 0] == obs[:, :5].argmax(1)).float().mean() > 0.9
     # SB2's RMSProp slot starts at 1 (small first steps), so A2C needs ~1000 updates here
     assert model.logs[-1]["ep_reward_mean"] > 6.5 > 3.0 > model.logs[1]["ep_reward_mean"]
+
+
+def test_ppo_loss_matches_numpy_restatement():
+    """ppo_loss against SB2 PPO2's loss written out in numpy (ppo2.py setup_model / _train_step)."""
+    from gym_futbol_amd.ppo import ppo_loss
+    torch.manual_seed(0)
+    pol = ActorCritic(6, [5, 3], [dict(pi=[8], vf=[8])])
+    rng = np.random.default_rng(1)
+    n = 64
+    obs = torch.as_tensor(rng.normal(size=(n, 6)))
+    act = torch.as_tensor(np.stack([rng.integers(0, 5, n), rng.integers(0, 3, n)], 1))
+    ret, val = torch.as_tensor(rng.normal(size=n) * 3), torch.as_tensor(rng.normal(size=n))
+    nlp_old = torch.as_tensor(rng.uniform(1.0, 3.0, n))
+    clip, clip_vf, ent_c, vf_c = 0.2, 0.2, 0.01, 0.5
+    loss, parts = ppo_loss(pol, obs, act, ret, val, nlp_old, clip, clip_vf, ent_c, vf_c)
+    with torch.no_grad():
+        logits, v = pol(obs)
+    lg, v = logits.double().numpy(), v.double().numpy()
+    R, V, NLP0 = ret.numpy(), val.numpy(), nlp_old.numpy()
+
+    def logsoftmax(x):
+        m = x.max(1, keepdims=True)
+        return x - m - np.log(np.exp(x - m).sum(1, keepdims=True))
+    l0, l1 = logsoftmax(lg[:, :5]), logsoftmax(lg[:, 5:])
+    a = act.numpy()
+    nlp = -(l0[np.arange(n), a[:, 0]] + l1[np.arange(n), a[:, 1]])
+    ent = -(np.exp(l0) * l0).sum(1) - (np.exp(l1) * l1).sum(1)
+    advs = R - V
+    advs = (advs - advs.mean()) / (advs.std() + 1e-8)
+    vclip = V + np.clip(v - V, -clip_vf, clip_vf)
+    vf_loss = 0.5 * np.mean(np.maximum((v - R) ** 2, (vclip - R) ** 2))
+    ratio = np.exp(NLP0 - nlp)
+    pg_loss = np.mean(np.maximum(-advs * ratio, -advs * np.clip(ratio, 1 - clip, 1 + clip)))
+    expect = pg_loss - ent.mean() * ent_c + vf_loss * vf_c
+    assert abs(float(loss.detach()) - expect) < 1e-5 * max(1.0, abs(expect))
+    p = parts.numpy()
+    assert np.allclose(p[:3], [pg_loss, vf_loss, ent.mean()], rtol=1e-5, atol=1e-6)
+    assert abs(p[3] - 0.5 * np.mean((nlp - NLP0) ** 2)) < 1e-5
+    assert abs(p[4] - np.mean(np.abs(ratio - 1) > clip)) < 1e-6
