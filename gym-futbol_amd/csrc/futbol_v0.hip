@@ -239,8 +239,12 @@ __device__ __forceinline__ void opp_team(const Ctx& c, Env& e)
         double v1x, v1y, v2x, v2y;
         const double m1 = get_vec(nb[0], nb[1], o1[0], o1[1], v1x, v1y);
         const double m2 = get_vec(nb[0], nb[1], o2[0], o2[1], v2x, v2y);
-        if (m1 < STEP_SIZE * P->player_speed) { o1[2] = v1x; o1[3] = v1y; o1[4] = m1 / STEP_SIZE; }
-        else if (m2 < STEP_SIZE * P->player_speed) { o2[2] = v2x; o2[3] = v2y; o2[4] = m2 / STEP_SIZE; }
+        // selects rather than if / else-if: the branchy form lets the compiler sink the three
+        // stores behind a select of row pointers, which demotes those rows to scratch
+        const bool u1 = m1 < STEP_SIZE * P->player_speed, u2 = !u1 && m2 < STEP_SIZE * P->player_speed;
+        const double s1 = m1 / STEP_SIZE, s2 = m2 / STEP_SIZE;
+        o1[2] = u1 ? v1x : o1[2]; o1[3] = u1 ? v1y : o1[3]; o1[4] = u1 ? s1 : o1[4];
+        o2[2] = u2 ? v2x : o2[2]; o2[3] = u2 ? v2y : o2[3]; o2[4] = u2 ? s2 : o2[4];
     }
 }
 
