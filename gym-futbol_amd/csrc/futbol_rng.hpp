@@ -79,9 +79,10 @@ struct Stream {
         return a + (b - a) * u;
     }
     // np.random.normal(mu, sigma): Box-Muller on one block
-    __host__ __device__ inline double normal(double mu, double sigma)
+    __host__ __device__ inline double normal(double mu, double sigma) { return normal_of(next(), mu, sigma); }
+    // the same from an already drawn block (the v0 kernel draws it in order and transforms it later)
+    __host__ __device__ static inline double normal_of(const Philox4& p, double mu, double sigma)
     {
-        const Philox4 p = next();
         const double a = u53(p.x[0], p.x[1]);
         const double b = u53(p.x[2], p.x[3]);
         const double z = sqrt(-2.0 * pm_log(1.0 - a)) * pm_cos(6.283185307179586 * b);

@@ -32,6 +32,11 @@ struct Env {
     uint32_t owner, last_owner;
     bool views_live;
     bool pending_done;
+    // a shot whose direction is still to be computed (resolve_shot): at most one agent holds the
+    // ball when it shoots, so the transcendental part runs once per step, not once per agent
+    bool shot;
+    Philox4 shot_p;
+    double shot_cs, shot_sn, shot_mag, shot_acc;
 };
 
 // get_vec (:62-65): vector from o to t and its magnitude
@@ -95,6 +100,7 @@ __device__ __forceinline__ void set_vector_observation(const Ctx& c, Env& e, boo
         if (action == INTERCEPT) {
             ag[2] = 0; ag[3] = 0; ag[4] = 0;
             ball[2] = 0; ball[3] = 0; ball[4] = 0;
+            e.shot = false;
         } else if (action == RUN) {
             ag[4] = P->player_speed;
             if (set_target) {
@@ -110,22 +116,22 @@ __device__ __forceinline__ void set_vector_observation(const Ctx& c, Env& e, boo
             else {
 #pragma unroll
                 for (int f = 0; f < 5; ++f) ball[f] = ag[f];
+                e.shot = false;
             }
         } else if (action == SHOOT) {
             const int acc = 10 + defence_near<a>(c, e) * 20;
             ball[4] = c.rs->randint(P->shoot_lo, P->shoot_hi) * 1.0;
             double vx, vy;
             const double mag = get_vec(right ? 0.0 : P->length, target_y, ball[0], ball[1], vx, vy);
-            // screw_vec (:101-116): one normal draw, then randint(0, 9) for the index
-            const double nd = c.rs->normal(0.0, (double)acc);
-            const double cs = vx * 1.0 / mag, sn = vy * 1.0 / mag;
+            // screw_vec (:101-116): one normal draw, then randint(0, 9) for the index; the
+            // rotation (Box-Muller, sin/cos) is applied by resolve_shot before the ball moves
+            e.shot_p = c.rs->next();
+            e.shot_acc = (double)acc;
+            e.shot_cs = vx * 1.0 / mag;
+            e.shot_sn = vy * 1.0 / mag;
+            e.shot_mag = mag;
+            e.shot = true;
             (void)c.rs->randint(0, 9);
-            const double ang = (nd / 180) * 3.141592653589793;
-            double ss, sc;
-            cr_sincos(ang, &ss, &sc);
-            const double tc = (cs * sc) - (sn * ss), ts = (sn * sc) + (cs * ss);
-            ball[2] = tc * mag;
-            ball[3] = ts * mag;
             e.last_owner = e.owner;
             e.owner = NOONE;
             ag[2] = 0; ag[3] = 0; ag[4] = 0;
@@ -138,6 +144,7 @@ __device__ __forceinline__ void set_vector_observation(const Ctx& c, Env& e, boo
             ball[4] = c.rs->uniform(cps - 1, cps + 1);
             ball[2] = vx;
             ball[3] = vy;
+            e.shot = false;
             e.last_owner = e.owner;
             e.owner = NOONE;
             ag[2] = 0; ag[3] = 0; ag[4] = 0;
@@ -151,6 +158,7 @@ __device__ __forceinline__ void set_vector_observation(const Ctx& c, Env& e, boo
             if (success || (e.owner == NOONE && btam < 2 + 2)) {
                 ball[2] = ag[2]; ball[3] = ag[3]; ball[4] = ag[4];
                 ball[0] = ag[0]; ball[1] = ag[1];
+                e.shot = false;
                 e.last_owner = e.owner;
                 e.owner = a;
             }
@@ -196,6 +204,24 @@ __device__ __forceinline__ void step_by_observation(double* o)
         o[0] = o[0] + o[4] * (tx * STEP_SIZE / mag);
         o[1] = o[1] + o[4] * (ty * STEP_SIZE / mag);
     }
+}
+
+// the deferred part of a shot (:362-381, screw_vec :101-116): nothing between the shot and
+// the ball's _step_by_observation reads the ball's direction -- later agents either leave it or
+// overwrite it (which cancels the pending shot), and the opponents' ball anticipation only runs
+// when neither opponent's action was SHOOT
+__device__ __forceinline__ void resolve_shot(Env& e)
+{
+    if (!e.shot) return;
+    const double nd = Stream::normal_of(e.shot_p, 0.0, e.shot_acc);
+    const double ang = (nd / 180) * 3.141592653589793;
+    double ss, sc;
+    cr_sincos(ang, &ss, &sc);
+    const double cs = e.shot_cs, sn = e.shot_sn;
+    const double tc = (cs * sc) - (sn * ss), ts = (sn * sc) + (cs * ss);
+    e.r[BALL][2] = tc * e.shot_mag;
+    e.r[BALL][3] = ts * e.shot_mag;
+    e.shot = false;
 }
 
 // _opp_team_set_vector_observation (:864-983)
@@ -356,6 +382,7 @@ __device__ __forceinline__ void load(const V0Ptrs& st, int env, int B, Env& e, M
     e.last_owner = m.last_owner();
     e.views_live = m.bit(kViewsLive);
     e.pending_done = false;
+    e.shot = false;
 }
 
 __device__ __forceinline__ void store(const V0Ptrs& st, int env, int B, const Env& e, Meta& m, bool row_valid)
@@ -430,6 +457,7 @@ __global__ void __launch_bounds__(64) v0_step_kernel(const V0Params* __restrict_
     }
     set_vector_observation<AI_1>(c, e, e.owner == AI_1, a0, false, 0, 0);
     set_vector_observation<AI_2>(c, e, e.owner == AI_2, a1, false, 0, 0);
+    resolve_shot(e);
 #pragma unroll
     for (int r = 0; r < 5; ++r) step_by_observation(e.r[r]);
 
