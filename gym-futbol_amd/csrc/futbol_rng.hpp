@@ -59,25 +59,37 @@ struct Stream {
 
     __host__ __device__ inline Philox4 next() { return philox4x32_10(j++, event, env, tag, k0, k1); }
 
-    __host__ __device__ inline double uniform01()
+    // the blocks of the next n draws, without consuming them (the v0 kernel computes them at a
+    // converged point and lets each exclusive branch take its draws by position; skip() then
+    // consumes what the lane's branch used)
+    template <int n>
+    __host__ __device__ inline void lookahead(Philox4 (&b)[n]) const
     {
-        const Philox4 p = next();
-        return u53(p.x[0], p.x[1]);
+#pragma unroll
+        for (int i = 0; i < n; ++i) b[i] = philox4x32_10(j + (uint32_t)i, event, env, tag, k0, k1);
     }
+    __host__ __device__ inline void skip(uint32_t n) { j += n; }
+
+    __host__ __device__ static inline double uniform01_of(const Philox4& p) { return u53(p.x[0], p.x[1]); }
     // random.choice over n items / gym MultiDiscrete.sample for one component
-    __host__ __device__ inline int choice(int n)
+    __host__ __device__ static inline int choice_of(const Philox4& p, int n)
     {
-        const double u = uniform01();
+        const double u = uniform01_of(p);
         int k = (int)floor(u * (double)n);
         return k > n - 1 ? n - 1 : k;
     }
-    __host__ __device__ inline int randint(int a, int b) { return a + choice(b - a + 1); }
+    __host__ __device__ static inline int randint_of(const Philox4& p, int a, int b) { return a + choice_of(p, b - a + 1); }
     // CPython random.uniform: a + (b - a) * random()
-    __host__ __device__ inline double uniform(double a, double b)
+    __host__ __device__ static inline double uniform_of(const Philox4& p, double a, double b)
     {
-        const double u = uniform01();
+        const double u = uniform01_of(p);
         return a + (b - a) * u;
     }
+
+    __host__ __device__ inline double uniform01() { return uniform01_of(next()); }
+    __host__ __device__ inline int choice(int n) { return choice_of(next(), n); }
+    __host__ __device__ inline int randint(int a, int b) { return randint_of(next(), a, b); }
+    __host__ __device__ inline double uniform(double a, double b) { return uniform_of(next(), a, b); }
     // np.random.normal(mu, sigma): Box-Muller on one block
     __host__ __device__ inline double normal(double mu, double sigma) { return normal_of(next(), mu, sigma); }
     // the same from an already drawn block (the v0 kernel draws it in order and transforms it later)

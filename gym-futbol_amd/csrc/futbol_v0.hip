@@ -95,7 +95,13 @@ __device__ __forceinline__ void set_vector_observation(const Ctx& c, Env& e, boo
     const V0Params* P = c.P;
     double* ag = e.r[a];
     double* ball = e.r[BALL];
-    const double target_y = (double)c.rs->randint(P->ty_lo, P->ty_hi);
+    // every path draws target_y first and then at most three more (shoot): the four blocks are
+    // computed here, where the wave is converged, and each exclusive branch takes its draws by
+    // position -- one Philox per draw position instead of one per draw site
+    Philox4 blk[4];
+    c.rs->lookahead(blk);
+    uint32_t used = 1;
+    const double target_y = (double)Stream::randint_of(blk[0], P->ty_lo, P->ty_hi);
     if (has_ball) {
         if (action == INTERCEPT) {
             ag[2] = 0; ag[3] = 0; ag[4] = 0;
@@ -112,7 +118,8 @@ __device__ __forceinline__ void set_vector_observation(const Ctx& c, Env& e, boo
                 ag[2] = vx;
                 ag[3] = vy;
             }
-            if (c.rs->uniform01() < 0.05) e.owner = NOONE;
+            used = 2;
+            if (Stream::uniform01_of(blk[1]) < 0.05) e.owner = NOONE;
             else {
 #pragma unroll
                 for (int f = 0; f < 5; ++f) ball[f] = ag[f];
@@ -120,18 +127,18 @@ __device__ __forceinline__ void set_vector_observation(const Ctx& c, Env& e, boo
             }
         } else if (action == SHOOT) {
             const int acc = 10 + defence_near<a>(c, e) * 20;
-            ball[4] = c.rs->randint(P->shoot_lo, P->shoot_hi) * 1.0;
+            ball[4] = Stream::randint_of(blk[1], P->shoot_lo, P->shoot_hi) * 1.0;
             double vx, vy;
             const double mag = get_vec(right ? 0.0 : P->length, target_y, ball[0], ball[1], vx, vy);
             // screw_vec (:101-116): one normal draw, then randint(0, 9) for the index; the
             // rotation (Box-Muller, sin/cos) is applied by resolve_shot before the ball moves
-            e.shot_p = c.rs->next();
+            e.shot_p = blk[2];
             e.shot_acc = (double)acc;
             e.shot_cs = vx * 1.0 / mag;
             e.shot_sn = vy * 1.0 / mag;
             e.shot_mag = mag;
             e.shot = true;
-            (void)c.rs->randint(0, 9);
+            used = 4;  // blk[3]: randint(0, 9), drawn and unused
             e.last_owner = e.owner;
             e.owner = NOONE;
             ag[2] = 0; ag[3] = 0; ag[4] = 0;
@@ -141,7 +148,8 @@ __device__ __forceinline__ void set_vector_observation(const Ctx& c, Env& e, boo
             const double mag = get_vec(mate[0], mate[1], ball[0], ball[1], vx, vy);
             double cps = mag / STEP_SIZE;
             if (cps > SHOOT_SPEED) cps = SHOOT_SPEED;
-            ball[4] = c.rs->uniform(cps - 1, cps + 1);
+            ball[4] = Stream::uniform_of(blk[1], cps - 1, cps + 1);
+            used = 2;
             ball[2] = vx;
             ball[3] = vy;
             e.shot = false;
@@ -154,7 +162,8 @@ __device__ __forceinline__ void set_vector_observation(const Ctx& c, Env& e, boo
         const double btam = get_vec(ball[0], ball[1], ag[0], ag[1], btax, btay);
         get_vec(right ? 0.0 : P->length, P->width / 2, ag[0], ag[1], gtax, gtay);
         if (action == INTERCEPT) {
-            const bool success = c.rs->uniform01() < intercept_chance(btam);
+            const bool success = Stream::uniform01_of(blk[1]) < intercept_chance(btam);
+            used = 2;
             if (success || (e.owner == NOONE && btam < 2 + 2)) {
                 ball[2] = ag[2]; ball[3] = ag[3]; ball[4] = ag[4];
                 ball[0] = ag[0]; ball[1] = ag[1];
@@ -171,6 +180,7 @@ __device__ __forceinline__ void set_vector_observation(const Ctx& c, Env& e, boo
             ag[2] = 0; ag[3] = 0; ag[4] = 0;
         }
     }
+    c.rs->skip(used);
 }
 
 // Easy_Agent.get_action_type (easy_agent.py:53-98), shoot_range = 20 (futbol_env.py:196-201)
