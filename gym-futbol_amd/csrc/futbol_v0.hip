@@ -95,10 +95,11 @@ __device__ __forceinline__ void set_vector_observation(const Ctx& c, Env& e, boo
     const V0Params* P = c.P;
     double* ag = e.r[a];
     double* ball = e.r[BALL];
-    // every path draws target_y first and then at most three more (shoot): the four blocks are
+    // every path draws target_y first and then at most three more (shoot): the blocks are
     // computed here, where the wave is converged, and each exclusive branch takes its draws by
-    // position -- one Philox per draw position instead of one per draw site
-    Philox4 blk[4];
+    // position -- one Philox per draw position instead of one per draw site.  The fourth
+    // (shoot's randint(0, 9)) only advances the counter: its value is never used
+    Philox4 blk[3];
     c.rs->lookahead(blk);
     uint32_t used = 1;
     const double target_y = (double)Stream::randint_of(blk[0], P->ty_lo, P->ty_hi);
@@ -138,7 +139,7 @@ __device__ __forceinline__ void set_vector_observation(const Ctx& c, Env& e, boo
             e.shot_sn = vy * 1.0 / mag;
             e.shot_mag = mag;
             e.shot = true;
-            used = 4;  // blk[3]: randint(0, 9), drawn and unused
+            used = 4;  // + randint(0, 9) (screw_vec's index): drawn, value unused
             e.last_owner = e.owner;
             e.owner = NOONE;
             ag[2] = 0; ag[3] = 0; ag[4] = 0;
