@@ -43,7 +43,16 @@ constexpr double kPlayerR = 1.5, kBallR = 1.0, kSegR = 1.0;
 constexpr double kPlayerMinv = 1.0 / 20.0, kBallMinv = 1.0 / 10.0;
 constexpr double kPlayerVmax = 10.0, kBallVmax = 25.0;
 constexpr double kE = 0.2;  // elasticity of players and ball; segments 0
-constexpr int CK = 4;       // arbiter-cache entries preloaded into registers
+// arbiter-cache entries preloaded into registers (5v5 / 10v10 envs hold more cached arbiters:
+// a lane with more than CK entries sends its whole wave through the global lookup loops)
+#ifndef FUTBOL_CK5
+#define FUTBOL_CK5 8
+#endif
+template <int N>
+constexpr int CKN = N >= 5 ? FUTBOL_CK5 : 4;
+// entries beyond CKN read per batch of independent loads (5v5 and up: registers are exhausted)
+template <int N>
+constexpr int CBN = N >= 5 ? 1 : 4;
 
 // Diagnostic build only (-DFUTBOL_STAMPS, bench.py --stamps): per-wave s_memtime at phase
 // boundaries, accumulated into st.stamps[wave][slot].  Never compiled into the product.
@@ -468,12 +477,12 @@ __device__ __forceinline__ bool far_from_segments(double x, double y, double rea
 // unconditionally (c < CK <= P is always in bounds) so that the loads carry no dependence on
 // ncache and can be issued together with the body state at the top of the kernel
 template <int N, int EPW>
-__device__ __forceinline__ void load_cache_pre(const Lane<N, EPW>& L, uint32_t ncache, uint32_t (&ck)[CK],
-                                               double (&cj)[CK])
+__device__ __forceinline__ void load_cache_pre(const Lane<N, EPW>& L, uint32_t ncache, uint32_t (&ck)[CKN<N>],
+                                               double (&cj)[CKN<N>])
 {
-    static_assert(CK <= V1Shape<N>::P, "preloaded cache entries must lie inside the [P][B] arrays");
+    static_assert(CKN<N> <= V1Shape<N>::P, "preloaded cache entries must lie inside the [P][B] arrays");
 #pragma unroll
-    for (int c = 0; c < CK; ++c) {
+    for (int c = 0; c < CKN<N>; ++c) {
         const uint32_t k = L.ckey[(size_t)c * L.B + L.env];
         const double j = L.cjn[(size_t)c * L.B + L.env];
         ck[c] = (uint32_t)c < ncache ? k : 0xffffu;
@@ -484,7 +493,7 @@ __device__ __forceinline__ void load_cache_pre(const Lane<N, EPW>& L, uint32_t n
 // ck / cj: the preloaded cache entries (load_cache_pre) of the env's CURRENT cache
 template <int N, int EPW>
 __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>& L, Env<N>& e, int dtc,
-                                           const uint32_t (&ck)[CK], const double (&cj)[CK]
+                                           const uint32_t (&ck)[CKN<N>], const double (&cj)[CKN<N>]
 #ifdef FUTBOL_STAMPS
                                            , unsigned long long* st_stamps, unsigned long long& _stamp_prev
 #endif
@@ -544,7 +553,7 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
         double jn = 0.0;
         bool normal = false;
 #pragma unroll
-        for (int c = 0; c < CK; ++c)
+        for (int c = 0; c < CKN<N>; ++c)
             if ((int)(ck[c] & 0x3ffu) == pair) {
                 jn = cj[c];
                 normal = (ck[c] >> 12) == 0;  // touched by the previous step: NORMAL -> warm start
@@ -660,23 +669,31 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
 
     FUTBOL_CRUMB(L, 40 + dtc);
     FUTBOL_STAMP(dtc == 2 ? 4 : 9);
-    // cache entries beyond the preloaded ones (rare): look them up in global memory
-    if (ncache > (uint32_t)CK) {
-        for (int s = 0; s < n; ++s) {
-            const int info = L.get_info(s);
-            const int pair = (info >> 11) & 511;
-            bool pre = false;
+    // cache entries beyond the preloaded ones: read in batches of CBN independent loads, each
+    // batch matched against every contact of this step.  Pairs are unique in the cache and among
+    // the contacts (survivors are the entries no contact touched), so a contact matches at most
+    // one entry, and none beyond CK if it matched a preloaded one.
+    if (ncache > (uint32_t)CKN<N>) {
+        for (uint32_t c0 = CKN<N>; c0 < ncache; c0 += CBN<N>) {
+            uint32_t key[CBN<N>];
+            double jn[CBN<N>];
 #pragma unroll
-            for (int c = 0; c < CK; ++c) pre |= (int)(ck[c] & 0x3ffu) == pair;
-            if (pre) continue;
-            for (uint32_t c = CK; c < ncache; ++c) {
-                const uint32_t key = L.ckey[(size_t)c * B + env];
-                if ((int)(key & 0x3ffu) == pair) {
-                    const double2 r2 = L.get(s, 2);
-                    L.put(s, 3, make_double2(L.cjn[(size_t)c * B + env], 0.0));
-                    if ((key >> 12) == 0)
-                        L.put(s, 2, make_double2(r2.x, __longlong_as_double(__double_as_longlong(r2.y) | (1ll << 20))));
-                    break;
+            for (int i = 0; i < CBN<N>; ++i) {
+                const uint32_t c = c0 + i < (uint32_t)S::P ? c0 + i : (uint32_t)S::P - 1;  // in bounds
+                const uint32_t k = L.ckey[(size_t)c * B + env];
+                jn[i] = L.cjn[(size_t)c * B + env];
+                key[i] = c0 + i < ncache ? k : 0xffffu;
+            }
+            for (int s = 0; s < n; ++s) {
+                const int pair = (L.get_info(s) >> 11) & 511;
+#pragma unroll
+                for (int i = 0; i < CBN<N>; ++i) {
+                    if ((int)(key[i] & 0x3ffu) == pair) {
+                        const double2 r2 = L.get(s, 2);
+                        L.put(s, 3, make_double2(jn[i], 0.0));
+                        if ((key[i] >> 12) == 0)
+                            L.put(s, 2, make_double2(r2.x, __longlong_as_double(__double_as_longlong(r2.y) | (1ll << 20))));
+                    }
                 }
             }
         }
@@ -818,7 +835,7 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
     // cpSpaceArbiterSetFilter + store jnAcc: survivors (untouched, age+1 < 3) then this step's contacts
     uint32_t w = 0;
 #pragma unroll
-    for (int c = 0; c < CK; ++c) {
+    for (int c = 0; c < CKN<N>; ++c) {
         if ((uint32_t)c < ncache) {
             const uint32_t key = ck[c], age = key >> 12;
             if (!((touched >> c) & 1u) && age + 1 < 3) {
@@ -830,18 +847,32 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
             }
         }
     }
-    for (uint32_t c = CK; c < ncache; ++c) {
-        const uint32_t key = L.ckey[(size_t)c * B + env];
-        const int pair = (int)(key & 0x3ffu);
-        const uint32_t age = key >> 12;
-        bool t = false;
-        for (int s = 0; s < n; ++s) t |= ((L.get_info(s) >> 11) & 511) == pair;
-        if (!t && age + 1 < 3) {
-            FB_BOUND(L, w < (uint32_t)S::P, 6, w = S::P - 1);
-            L.cjn[(size_t)w * B + env] = L.cjn[(size_t)c * B + env];
-            FB_BOUND(L, w < (uint32_t)S::P, 6, w = S::P - 1);
-            L.ckey[(size_t)w * B + env] = (uint16_t)(pair | ((age + 1) << 12));
-            ++w;
+    // (batches of CBN loads; in-place compaction is safe: w <= c for every entry c, and a batch
+    // is loaded before any of its survivors is written)
+    for (uint32_t c0 = CKN<N>; c0 < ncache; c0 += CBN<N>) {
+        uint32_t key[CBN<N>];
+        double jn[CBN<N>];
+#pragma unroll
+        for (int i = 0; i < CBN<N>; ++i) {
+            const uint32_t c = c0 + i < (uint32_t)S::P ? c0 + i : (uint32_t)S::P - 1;
+            key[i] = L.ckey[(size_t)c * B + env];
+            jn[i] = L.cjn[(size_t)c * B + env];
+        }
+#pragma unroll
+        for (int i = 0; i < CBN<N>; ++i) {
+            if (c0 + i < ncache) {
+                const int pair = (int)(key[i] & 0x3ffu);
+                const uint32_t age = key[i] >> 12;
+                bool t = false;
+                for (int s = 0; s < n; ++s) t |= ((L.get_info(s) >> 11) & 511) == pair;
+                if (!t && age + 1 < 3) {
+                    FB_BOUND(L, w < (uint32_t)S::P, 6, w = S::P - 1);
+                    L.cjn[(size_t)w * B + env] = jn[i];
+                    FB_BOUND(L, w < (uint32_t)S::P, 6, w = S::P - 1);
+                    L.ckey[(size_t)w * B + env] = (uint16_t)(pair | ((age + 1) << 12));
+                    ++w;
+                }
+            }
         }
     }
     for (int s = 0; s < n; ++s) {
@@ -954,8 +985,8 @@ __device__ __forceinline__ void do_reset(const V1Params& P, const V1Params* __re
     e.meta.set_owner((uint32_t)rs.choice(2));
     e.meta.set_steps(0);
     position_to_initial<N>(P, e);
-    uint32_t ck[CK];
-    double cj[CK];
+    uint32_t ck[CKN<N>];
+    double cj[CKN<N>];
     load_cache_pre<N, EPW>(L, e.meta.ncache(), ck, cj);
     space_step<N, EPW>(P, L, e, 1, ck, cj
 #ifdef FUTBOL_STAMPS
@@ -1047,8 +1078,8 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
     // (one memory round trip per step)
     Env<N> e;
     load_env<N>(st, env, B, e);
-    uint32_t ck[CK];
-    double cj[CK];
+    uint32_t ck[CKN<N>];
+    double cj[CKN<N>];
     load_cache_pre<N, EPW>(L, e.meta.ncache(), ck, cj);
     const double ep_ret0 = st.ep_ret[env];
     // the left team's actions: 2N bytes per env, as 32-bit words when 2N % 4 == 0 (rows stay
