@@ -132,20 +132,30 @@ struct Scratch {
     using S = V1Shape<N>;
     // LDS contact slots per lane: the same at every EPW, so that 64/EPW times as many blocks fit per CU
     static constexpr int K = S::K;
-    // contact record s of lane l: rec[s][0][l] = (nx, ny), [1] = (nMass, bias),
-    // [2] = (bounce, info bits), [3] = (jnAcc, jBias): four ds_read_b128 per record
+    // contact record s of lane l: rec[s][0][l] = (nx, ny), [1] = (nMass, info bits),
+    // [2] = (bias, -bounce), [3] = (jBias, jnAcc): element h of [2] / [3] belongs to half h of
+    // the split solve (h = 0: v_bias / jBias chain, h = 1: v / jnAcc chain)
     double2 rec[K][4][EPW];
-    // body velocity / v_bias during the solve; v row Nb is the static body (segments) and
-    // the target of null records: it stays exactly +0.0 (its inverse mass is 0), and it also
-    // serves as the static body's v_bias row (vrow_of / brow_of)
-    double2 v[S::Nb + 1][EPW];
-    double2 vb[S::Nb][EPW];
+    // solver rows, one double2 per body and lane: rows[k] = body k's v_bias (k < Nb),
+    // rows[Nb] = the static body Z (v = v_bias = +0 forever: its inverse mass is 0), rows[2 Nb - k]
+    // = body k's v.  A record's row offset off = k * ROW (Z: Nb * ROW) addresses half h's row
+    // as rows[0] + off (h = 0) or rows[2 Nb] - off (h = 1): both halves reach Z with no select.
+    // During the narrowphase the same rows stage the bodies' positions (v_bias rows) and
+    // velocities (v rows) for the per-lane dynamic body index.
+    double2 rows[2 * S::Nb + 1][EPW];
+    double minv[S::Nb + 1];  // inverse mass by row: players, ball, Z = 0
+    uint8_t item_env[EPW];   // split solve: compacted list of the lanes (envs) with contacts
+    uint16_t item_n[EPW];    // ... and their record counts
+    uint8_t item_pc[EPW];    // ... and the dt code of their previous cpSpaceStep (warm-start dt ratio)
     SegLds seg[kNSeg];
+
+    __device__ __forceinline__ double2& vb(int k, int l) { return rows[k][l]; }
+    __device__ __forceinline__ double2& v(int k, int l) { return rows[2 * S::Nb - k][l]; }
 };
 
 // info word (64 bits, stored as the bits of a double):
 //   low 32: a (5 bits) | bcode (6 bits: body id, or 32 + segment) << 5 | pair << 11 | normal << 20
-//   high 32: byte offset of a's solver row | byte offset of b's row (static row for segments) << 16,
+//   high 32: row offset of a (k * ROW) | row offset of b (Nb * ROW = Z for segments) << 16,
 //            filled in by with_rows() in the solver prologue (not at the many collide sites:
 //            constants hoisted out of them cost registers)
 __device__ __forceinline__ long long pack_info(int a, int bcode, int pair, bool normal)
@@ -169,7 +179,8 @@ __device__ __forceinline__ long long null_info()
     return (long long)(((unsigned long long)(R | (R << 16)) << 32));
 }
 
-// global spill record (slot s >= K): 8 doubles [nx, ny, nMass, bias, bounce, info, jnAcc, jBias]
+// global spill record (slot s >= K): 8 doubles [nx, ny, nMass, info, bias, -bounce, jBias, jnAcc]
+// (the LDS record's four double2 in order), at spill[(s - K) * 8 + f][env]
 template <int N, int EPW>
 struct Lane {
     using S = V1Shape<N>;
@@ -206,155 +217,52 @@ struct Lane {
             *sp(s, 2 * q + 1) = x.y;
         }
     }
-    __device__ __forceinline__ int get_info(int s) const { return (int)__double_as_longlong(get(s, 2).y); }
-    __device__ __forceinline__ double get_jn(int s) const { return get(s, 3).x; }
+    __device__ __forceinline__ int get_info(int s) const { return (int)__double_as_longlong(get(s, 1).y); }
+    __device__ __forceinline__ double get_jn(int s) const { return get(s, 3).y; }
     __device__ __forceinline__ void set_rec(int s, double nx, double ny, double nm, double bi, double bo, double j,
                                             long long info) const
     {
         put(s, 0, make_double2(nx, ny));
-        put(s, 1, make_double2(nm, bi));
-        put(s, 2, make_double2(bo, __longlong_as_double(info)));
-        put(s, 3, make_double2(j, 0.0));
+        put(s, 1, make_double2(nm, __longlong_as_double(info)));
+        put(s, 2, make_double2(bi, -bo));
+        put(s, 3, make_double2(0.0, j));
     }
 };
 
-// LDS address of a solver row from its byte offset (info): v rows directly, v_bias rows with
-// the static offset redirected to the (zero) static v row
-template <int N, int EPW>
-__device__ __forceinline__ double2* vrow_of(Scratch<N, EPW>* sh, int ln, uint32_t off)
+// One half of cpArbiterApplyImpulse for one contact (frictionless: players, ball and segments
+// have friction 0 except the segments' 1, and u = a.u * b.u = 0, so no tangent impulse and no
+// rotation).  The normal impulse's two accumulators are independent chains:
+//   h = 0: jbn = (bias - vbn) * nMass, jBias = max(jBias + jbn, 0), applied to v_bias;
+//   h = 1: jn = -(bounce + vrn) * nMass, jnAcc = max(jnAcc + jn, 0), applied to v,
+// with c = bias / -bounce from the record: (c - vn) * nMass.  For h = 1 this is
+// ((-bounce) - vrn) * nMass, which differs from -(bounce + vrn) * nMass at most in the sign of
+// a zero; jnAcc + (+-0) is the same double for every jnAcc >= +0, so the results are identical.
+// ra / rb: rows of a and b in this half (rb = Z for a segment: mb = 0 keeps it +0).
+__device__ __forceinline__ void apply_half(double2* ra, double2* rb, double nx, double ny, double nMass, double c,
+                                           double ma, double mb, double& acc)
 {
-    return (double2*)((char*)&sh->v[0][ln] + off);
-}
-template <int N, int EPW>
-__device__ __forceinline__ double2* brow_of(Scratch<N, EPW>* sh, int ln, uint32_t off)
-{
-    constexpr uint32_t SROW = (uint32_t)V1Shape<N>::Nb * EPW * (uint32_t)sizeof(double2);
-    return off == SROW ? &sh->v[V1Shape<N>::Nb][ln] : (double2*)((char*)&sh->vb[0][ln] + off);
-}
-
-// One contact of cpArbiterApplyImpulse (frictionless).  r0..r2 = the record's constant
-// part (normal, nMass, bias, bounce, info), r3 = (jnAcc, jBias), written back to *r3p.
-// Body rows come from the info offsets; a segment's b is the static row (v = v_bias = 0,
-// inverse mass 0: its updates add +-0 to +0 and leave it +0), which reproduces
-// Chipmunk's static-body arithmetic exactly without a branch.
-template <int N, int EPW>
-__device__ __forceinline__ void apply_contact(Scratch<N, EPW>* sh, int ln, double2 r0, double2 r1, double2 r2,
-                                              double2 r3, double2* r3p)
-{
-    using S = V1Shape<N>;
-    constexpr uint32_t ROW = EPW * (uint32_t)sizeof(double2);
-    const uint32_t offs = (uint32_t)((unsigned long long)__double_as_longlong(r2.y) >> 32);
-    const uint32_t ao = offs & 0xffffu, bo = offs >> 16;
-    double2* pva = vrow_of(sh, ln, ao);
-    double2* pvb = vrow_of(sh, ln, bo);
-    double2* pba = brow_of(sh, ln, ao);
-    double2* pbb = brow_of(sh, ln, bo);
-    const double2 va = *pva, ba = *pba, vbv = *pvb, bbv = *pbb;
-    const double nx = r0.x, ny = r0.y, nMass = r1.x, bias = r1.y, bounce = r2.x;
-    const double jnOld = r3.x, jbOld = r3.y;
-    const double vbn = (bbv.x - ba.x) * nx + (bbv.y - ba.y) * ny;
-    const double vrn = (vbv.x - va.x) * nx + (vbv.y - va.y) * ny;
-    const double jbn = (bias - vbn) * nMass;
-    const double tb = jbOld + jbn;
-    const double jb = tb > 0.0 ? tb : 0.0;
-    const double jnv = -(bounce + vrn) * nMass;
-    const double tn = jnOld + jnv;
-    const double jnAcc = tn > 0.0 ? tn : 0.0;
-    *r3p = make_double2(jnAcc, jb);
-    const double db = jb - jbOld, dj = jnAcc - jnOld;
-    const double jbx = nx * db, jby = ny * db, jx = nx * dj, jy = ny * dj;
-    const double ma = ao == (uint32_t)S::BALL * ROW ? kBallMinv : kPlayerMinv;
-    const double mb = bo == (uint32_t)S::BALL * ROW ? kBallMinv : (bo == (uint32_t)S::Nb * ROW ? 0.0 : kPlayerMinv);
-    *pba = make_double2(ba.x + (-jbx) * ma, ba.y + (-jby) * ma);
-    *pva = make_double2(va.x + (-jx) * ma, va.y + (-jy) * ma);
-    *pbb = make_double2(bbv.x + jbx * mb, bbv.y + jby * mb);
-    *pvb = make_double2(vbv.x + jx * mb, vbv.y + jy * mb);
+    const double2 va = *ra, vb = *rb;
+    const double vn = (vb.x - va.x) * nx + (vb.y - va.y) * ny;
+    const double j = (c - vn) * nMass;
+    const double old = acc;
+    const double t = old + j;
+    const double nacc = t > 0.0 ? t : 0.0;
+    acc = nacc;
+    const double d = nacc - old;
+    const double jx = nx * d, jy = ny * d;
+    *ra = make_double2(va.x + (-jx) * ma, va.y + (-jy) * ma);
+    *rb = make_double2(vb.x + jx * mb, vb.y + jy * mb);
 }
 
-// cpArbiterApplyCachedImpulse for one contact (only NORMAL arbiters are warm started)
-template <int N, int EPW>
-__device__ __forceinline__ void warm_contact(Scratch<N, EPW>* sh, int ln, double2 r0, double2 r2, double2 r3,
-                                             double dt_coef)
+// cpArbiterApplyCachedImpulse for one contact (v half; only NORMAL arbiters are warm started)
+__device__ __forceinline__ void warm_half(double2* ra, double2* rb, double nx, double ny, double jn, double dt_coef,
+                                          double ma, double mb)
 {
-    using S = V1Shape<N>;
-    constexpr uint32_t ROW = EPW * (uint32_t)sizeof(double2);
-    const unsigned long long info = (unsigned long long)__double_as_longlong(r2.y);
-    if (!((info >> 20) & 1)) return;
-    const uint32_t offs = (uint32_t)(info >> 32);
-    const uint32_t ao = offs & 0xffffu, bo = offs >> 16;
-    double2* pva = vrow_of(sh, ln, ao);
-    double2* pvb = vrow_of(sh, ln, bo);
-    const double jn = r3.x;
-    const double jx = (r0.x * jn) * dt_coef, jy = (r0.y * jn) * dt_coef;
-    const double ma = ao == (uint32_t)S::BALL * ROW ? kBallMinv : kPlayerMinv;
-    const double mb = bo == (uint32_t)S::BALL * ROW ? kBallMinv : (bo == (uint32_t)S::Nb * ROW ? 0.0 : kPlayerMinv);
-    const double2 va = *pva;
-    *pva = make_double2(va.x + (-jx) * ma, va.y + (-jy) * ma);
-    const double2 vbb = *pvb;
-    *pvb = make_double2(vbb.x + jx * mb, vbb.y + jy * mb);
-}
-
-// Register-resident form of apply_contact: the record's fields are scalars held across the
-// 10 iterations, only the body rows go through LDS.  DYN = false: b is the static row
-// (segment contact or null record) -- b's velocities are exactly +0 and stay so, hence
-// they are neither read nor written; the arithmetic is the DYN = true one with b = 0.
-template <int N, int EPW, bool DYN>
-__device__ __forceinline__ void apply_rows(Scratch<N, EPW>* sh, int ln, double nx, double ny, double nMass,
-                                           double bias, double bounce, uint32_t ao, uint32_t bo, double& jnAcc,
-                                           double& jBias)
-{
-    using S = V1Shape<N>;
-    constexpr uint32_t ROW = EPW * (uint32_t)sizeof(double2);
-    double2* pva = vrow_of(sh, ln, ao);
-    double2* pba = brow_of(sh, ln, ao);
-    const double2 va = *pva, ba = *pba;
-    double2 vbv = make_double2(0.0, 0.0), bbv = make_double2(0.0, 0.0);
-    double2 *pvb = nullptr, *pbb = nullptr;
-    if constexpr (DYN) {
-        pvb = vrow_of(sh, ln, bo);
-        pbb = brow_of(sh, ln, bo);
-        vbv = *pvb;
-        bbv = *pbb;
-    }
-    const double jnOld = jnAcc, jbOld = jBias;
-    const double vbn = (bbv.x - ba.x) * nx + (bbv.y - ba.y) * ny;
-    const double vrn = (vbv.x - va.x) * nx + (vbv.y - va.y) * ny;
-    const double jbn = (bias - vbn) * nMass;
-    const double tb = jbOld + jbn;
-    const double jb = tb > 0.0 ? tb : 0.0;
-    const double jnv = -(bounce + vrn) * nMass;
-    const double tn = jnOld + jnv;
-    const double jn = tn > 0.0 ? tn : 0.0;
-    jnAcc = jn;
-    jBias = jb;
-    const double db = jb - jbOld, dj = jn - jnOld;
-    const double jbx = nx * db, jby = ny * db, jx = nx * dj, jy = ny * dj;
-    const double ma = ao == (uint32_t)S::BALL * ROW ? kBallMinv : kPlayerMinv;
-    *pba = make_double2(ba.x + (-jbx) * ma, ba.y + (-jby) * ma);
-    *pva = make_double2(va.x + (-jx) * ma, va.y + (-jy) * ma);
-    if constexpr (DYN) {
-        const double mb = bo == (uint32_t)S::BALL * ROW ? kBallMinv : (bo == (uint32_t)S::Nb * ROW ? 0.0 : kPlayerMinv);
-        *pbb = make_double2(bbv.x + jbx * mb, bbv.y + jby * mb);
-        *pvb = make_double2(vbv.x + jx * mb, vbv.y + jy * mb);
-    }
-}
-
-template <int N, int EPW>
-__device__ __forceinline__ void warm_rows(Scratch<N, EPW>* sh, int ln, double nx, double ny, bool normal, uint32_t ao,
-                                          uint32_t bo, double jn, double dt_coef)
-{
-    using S = V1Shape<N>;
-    constexpr uint32_t ROW = EPW * (uint32_t)sizeof(double2);
-    if (!normal) return;
-    double2* pva = vrow_of(sh, ln, ao);
-    double2* pvb = vrow_of(sh, ln, bo);
     const double jx = (nx * jn) * dt_coef, jy = (ny * jn) * dt_coef;
-    const double ma = ao == (uint32_t)S::BALL * ROW ? kBallMinv : kPlayerMinv;
-    const double mb = bo == (uint32_t)S::BALL * ROW ? kBallMinv : (bo == (uint32_t)S::Nb * ROW ? 0.0 : kPlayerMinv);
-    const double2 va = *pva;
-    *pva = make_double2(va.x + (-jx) * ma, va.y + (-jy) * ma);
-    const double2 vbb = *pvb;
-    *pvb = make_double2(vbb.x + jx * mb, vbb.y + jy * mb);
+    const double2 va = *ra;
+    *ra = make_double2(va.x + (-jx) * ma, va.y + (-jy) * ma);
+    const double2 vb = *rb;
+    *rb = make_double2(vb.x + jx * mb, vb.y + jy * mb);
 }
 
 template <int N>
@@ -503,7 +411,6 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
     const double dt = dtc == 2 ? P.dtv[2] : P.dtv[1];
     const double rdt = dtc == 2 ? P.rdt[2] : P.rdt[1];
     const uint32_t pc = e.meta.dtcode();
-    const double prev_dt = pc == 2 ? P.dtv[2] : (pc == 1 ? P.dtv[1] : 0.0);
     const double biasCoef = dtc == 2 ? P.biasc[2] : P.biasc[1];
     const double damping = dtc == 2 ? P.damp[2] : P.damp[1];
     const double slop = P.slop, W = P.W, H = P.H;
@@ -533,8 +440,8 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
     const int ln_ = L.lane;
     sfor<S::Nb>([&](auto K) {
         constexpr int k = K;
-        sh_->vb[k][ln_] = make_double2(e.px[k], e.py[k]);
-        sh_->v[k][ln_] = make_double2(e.vx[k], e.vy[k]);
+        sh_->vb(k, ln_) = make_double2(e.px[k], e.py[k]);
+        sh_->v(k, ln_) = make_double2(e.vx[k], e.vy[k]);
     });
     // collide in canonical order; cpArbiterUpdate + preStep folded in (needs pre-damping v)
     int n = 0;
@@ -607,7 +514,7 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
             const int bi = bit / kNSeg;
             const int sg = bit - bi * kNSeg;
             const int i = i0 + bi;
-            const double2 pi_ = sh_->vb[i][ln_], vi = sh_->v[i][ln_];
+            const double2 pi_ = sh_->vb(i, ln_), vi = sh_->v(i, ln_);
             const bool ball = i == S::BALL;
             const double ri = ball ? kBallR : kPlayerR, mi = ball ? kBallMinv : kPlayerMinv;
             const SegLds g = sh_->seg[sg];
@@ -657,7 +564,7 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
         while (hits) {
             const int j = __builtin_ctz(hits);
             hits &= hits - 1;
-            const double2 pj = sh_->vb[j][ln_], vj = sh_->v[j][ln_];
+            const double2 pj = sh_->vb(j, ln_), vj = sh_->v(j, ln_);
             const bool ball_j = j == S::BALL;
             const double rj = ball_j ? kBallR : kPlayerR, mj = ball_j ? kBallMinv : kPlayerMinv;
             double nx, ny, p1x, p1y, p2x, p2y;
@@ -689,10 +596,10 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
 #pragma unroll
                 for (int i = 0; i < CBN<N>; ++i) {
                     if ((int)(key[i] & 0x3ffu) == pair) {
-                        const double2 r2 = L.get(s, 2);
-                        L.put(s, 3, make_double2(jn[i], 0.0));
+                        const double2 r1 = L.get(s, 1);
+                        L.put(s, 3, make_double2(0.0, jn[i]));
                         if ((key[i] >> 12) == 0)
-                            L.put(s, 2, make_double2(r2.x, __longlong_as_double(__double_as_longlong(r2.y) | (1ll << 20))));
+                            L.put(s, 1, make_double2(r1.x, __longlong_as_double(__double_as_longlong(r1.y) | (1ll << 20))));
                     }
                 }
             }
@@ -717,8 +624,16 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
 
     FUTBOL_STAMP(dtc == 2 ? 5 : 9);
     {
-        // wave-uniform record count over the LDS slots; lanes with fewer records are padded
-        // with null records, so the solver loop has no per-lane trip count
+        // Sequential-impulse solve (cpSpaceStep: warm start, then 10 iterations over the arbiters
+        // in canonical order), split in two independent halves per env -- the v_bias / jBias chain
+        // and the v / jnAcc chain (apply_half) -- and spread over the wave's active lanes: the
+        // envs with contacts are compacted into a work list of 2 C items (env, half), and lane w
+        // solves item w (then w + A, ... when 2 C exceeds the A active lanes).  Each item is one
+        // lane's serial chain of (10 + warm start) x records half-applications, so an env's
+        // critical path is half the instructions of a whole application, and lanes without
+        // contacts do the other halves.  Records live in LDS (lanes with fewer records than the
+        // wave's LDS maximum are padded with null records) and past the K LDS slots in the global
+        // spill area; rows and records of env e are column e of the block's LDS arrays.
         Scratch<N, EPW>* sh = L.sh;
         const int ln = L.lane;
         constexpr int KL = Lane<N, EPW>::KL;
@@ -735,98 +650,144 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
             atomicAdd(&st_stamps[(size_t)(blockIdx.x * EPW / 64) * 16 + 15], (unsigned long long)m);
 #endif
         if (m > 0) {
-            sfor<S::Nb>([&](auto K) {
-                constexpr int k = K;
-                sh->v[k][ln] = make_double2(e.vx[k], e.vy[k]);
-                sh->vb[k][ln] = make_double2(0.0, 0.0);
-            });
-            sh->v[S::Nb][ln] = make_double2(0.0, 0.0);
-            for (int s = 0; s < nf; ++s) {
-                const double2 r2 = sh->rec[s][2][ln];
-                sh->rec[s][2][ln] = make_double2(r2.x, __longlong_as_double(with_rows<N, EPW>(__double_as_longlong(r2.y))));
-            }
-            if (spill)
-                for (int s = KL; s < n; ++s) {
-                    const double2 r2 = L.get(s, 2);
-                    L.put(s, 2, make_double2(r2.x, __longlong_as_double(with_rows<N, EPW>(__double_as_longlong(r2.y)))));
-                }
-            for (int s = nf; s < m; ++s) {
-                sh->rec[s][0][ln] = make_double2(0.0, 0.0);
-                sh->rec[s][1][ln] = make_double2(0.0, 0.0);
-                sh->rec[s][2][ln] = make_double2(0.0, __longlong_as_double(null_info<N, EPW>()));
-                sh->rec[s][3][ln] = make_double2(0.0, 0.0);
-            }
-            const double dt_coef = (prev_dt == 0.0) ? 0.0 : dt / prev_dt;
-            // the first MR slots stay in registers for the whole solve (record, jnAcc, jBias);
-            // a slot whose b is static in every lane takes the branch-free static path
-            constexpr int MR = N <= 3 ? 4 : (N <= 5 ? 3 : 2);
-            constexpr uint32_t SROW = (uint32_t)S::Nb * EPW * (uint32_t)sizeof(double2);
-            double qnx[MR], qny[MR], qnm[MR], qbi[MR], qbo[MR], qjn[MR], qjb[MR];
-            uint32_t qa[MR], qb[MR];
-            bool qnorm[MR], qdyn[MR];
-            sfor<MR>([&](auto Q) {
-                constexpr int q = Q;
-                qdyn[q] = false;
-                if (q < m) {
-                    const double2 r0 = sh->rec[q][0][ln], r1 = sh->rec[q][1][ln], r2 = sh->rec[q][2][ln],
-                                  r3 = sh->rec[q][3][ln];
-                    const unsigned long long info = (unsigned long long)__double_as_longlong(r2.y);
-                    qnx[q] = r0.x;
-                    qny[q] = r0.y;
-                    qnm[q] = r1.x;
-                    qbi[q] = r1.y;
-                    qbo[q] = r2.x;
-                    qjn[q] = r3.x;
-                    qjb[q] = r3.y;
-                    qa[q] = (uint32_t)(info >> 32) & 0xffffu;
-                    qb[q] = (uint32_t)(info >> 48);
-                    qnorm[q] = (info >> 20) & 1;
-                    qdyn[q] = __ballot(qb[q] != SROW) != 0;
-                }
-            });
-            sfor<MR>([&](auto Q) {
-                constexpr int q = Q;
-                if (q < m) warm_rows<N, EPW>(sh, ln, qnx[q], qny[q], qnorm[q], qa[q], qb[q], qjn[q], dt_coef);
-            });
-            for (int s = MR; s < m; ++s)
-                warm_contact<N, EPW>(sh, ln, sh->rec[s][0][ln], sh->rec[s][2][ln], sh->rec[s][3][ln], dt_coef);
-            if (spill)
-                for (int s = KL; s < n; ++s) warm_contact<N, EPW>(sh, ln, L.get(s, 0), L.get(s, 2), L.get(s, 3), dt_coef);
-            for (int it = 0; it < 10; ++it) {
-                sfor<MR>([&](auto Q) {
-                    constexpr int q = Q;
-                    if (q < m) {
-                        if (qdyn[q])
-                            apply_rows<N, EPW, true>(sh, ln, qnx[q], qny[q], qnm[q], qbi[q], qbo[q], qa[q], qb[q],
-                                                     qjn[q], qjb[q]);
-                        else
-                            apply_rows<N, EPW, false>(sh, ln, qnx[q], qny[q], qnm[q], qbi[q], qbo[q], qa[q], qb[q],
-                                                      qjn[q], qjb[q]);
-                    }
+            // owner lanes (envs with contacts) publish their rows, row offsets and padding
+            const uint64_t act = __ballot(n > 0);
+            if (n > 0) {
+                sfor<S::Nb>([&](auto K) {
+                    constexpr int k = K;
+                    sh->v(k, ln) = make_double2(e.vx[k], e.vy[k]);
+                    sh->vb(k, ln) = make_double2(0.0, 0.0);
                 });
-                for (int s = MR; s < m; ++s)
-                    apply_contact<N, EPW>(sh, ln, sh->rec[s][0][ln], sh->rec[s][1][ln], sh->rec[s][2][ln],
-                                          sh->rec[s][3][ln], &sh->rec[s][3][ln]);
-                if (spill) {
-                    for (int s = KL; s < n; ++s) {
-                        double2 r3 = L.get(s, 3);
-                        apply_contact<N, EPW>(sh, ln, L.get(s, 0), L.get(s, 1), L.get(s, 2), r3, &r3);
-                        L.put(s, 3, r3);
+                sh->rows[S::Nb][ln] = make_double2(0.0, 0.0);
+                for (int s = 0; s < nf; ++s) {
+                    const double2 r1 = sh->rec[s][1][ln];
+                    sh->rec[s][1][ln] = make_double2(r1.x, __longlong_as_double(with_rows<N, EPW>(__double_as_longlong(r1.y))));
+                }
+                for (int s = KL; s < n; ++s) {
+                    const double2 r1 = L.get(s, 1);
+                    L.put(s, 1, make_double2(r1.x, __longlong_as_double(with_rows<N, EPW>(__double_as_longlong(r1.y)))));
+                }
+                for (int s = nf; s < m; ++s) {
+                    sh->rec[s][0][ln] = make_double2(0.0, 0.0);
+                    sh->rec[s][1][ln] = make_double2(0.0, __longlong_as_double(null_info<N, EPW>()));
+                    sh->rec[s][2][ln] = make_double2(0.0, 0.0);
+                    sh->rec[s][3][ln] = make_double2(0.0, 0.0);
+                }
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+                sh->item_env[rank] = (uint8_t)ln;
+                sh->item_n[rank] = (uint16_t)n;
+                sh->item_pc[rank] = (uint8_t)pc;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint64_t live = __ballot(1);
+            const int A = __popcll(live);
+            const int w = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
+            const int items = 2 * __popcll(act);
+            constexpr uint32_t ROW = EPW * (uint32_t)sizeof(double2);
+            for (int i0 = 0; i0 < items; i0 += A) {
+                const int it_ = i0 + w;
+                if (it_ < items) {
+                    const int ie = sh->item_env[it_ >> 1];
+                    const int h = it_ & 1;
+                    // cpArbiterApplyCachedImpulse's dt ratio of THIS env (its previous step may have
+                    // been a 1e-4 reset micro-step)
+                    const uint32_t ipc = sh->item_pc[it_ >> 1];
+                    const double iprev = ipc == 2 ? P.dtv[2] : (ipc == 1 ? P.dtv[1] : 0.0);
+                    const double dt_coef = (iprev == 0.0) ? 0.0 : dt / iprev;
+                    char* const base = (char*)&sh->rows[h ? 2 * S::Nb : 0][ie];
+                    const int sgn = h ? -1 : 1;
+                    const double* const mtab = sh->minv;
+                    auto row = [&](uint32_t off) { return (double2*)(base + sgn * (int)off); };
+                    auto mass = [&](uint32_t off) { return mtab[off / ROW]; };
+                    auto info_of = [&](double x) { return (unsigned long long)__double_as_longlong(x); };
+                    // the env's spill records (beyond the LDS slots): global, indexed by its env id
+                    const int ienv = env - ln + ie;
+                    auto spp = [&](int s, int f) {
+                        int t = s - KL;
+                        FB_BOUND(L, t >= 0 && t < S::P - KL, 0, t = 0);
+                        return L.spill + ((size_t)t * 8 + f) * B + ienv;
+                    };
+                    const int nie = spill ? (int)sh->item_n[it_ >> 1] : 0;  // env ie's record count
+                    // the env's LDS records in registers for the whole solve (m is wave-uniform: the
+                    // q < m guards are scalar branches): only the two body rows of each half-
+                    // application go through LDS on the serial chain
+                    double qnx[KL], qny[KL], qnm[KL], qc[KL], qacc[KL], qma[KL], qmb[KL];
+                    double2 *qra[KL], *qrb[KL];
+                    bool qwarm[KL];
+                    sfor<KL>([&](auto Q) {
+                        constexpr int q = Q;
+                        if (q < m) {
+                            const double2 r0 = sh->rec[q][0][ie], r1 = sh->rec[q][1][ie], r2 = sh->rec[q][2][ie],
+                                          r3 = sh->rec[q][3][ie];
+                            const unsigned long long info = info_of(r1.y);
+                            const uint32_t ao = (uint32_t)(info >> 32) & 0xffffu, bo = (uint32_t)(info >> 48);
+                            qnx[q] = r0.x;
+                            qny[q] = r0.y;
+                            qnm[q] = r1.x;
+                            qc[q] = h ? r2.y : r2.x;
+                            qacc[q] = h ? r3.y : r3.x;
+                            qra[q] = row(ao);
+                            qrb[q] = row(bo);
+                            qma[q] = mass(ao);
+                            qmb[q] = mass(bo);
+                            qwarm[q] = h && ((info >> 20) & 1);
+                        }
+                    });
+                    // warm start (cpArbiterApplyCachedImpulse), v half only, record order
+                    sfor<KL>([&](auto Q) {
+                        constexpr int q = Q;
+                        if (q < m && qwarm[q]) warm_half(qra[q], qrb[q], qnx[q], qny[q], qacc[q], dt_coef, qma[q], qmb[q]);
+                    });
+                    if (h) {
+                        for (int s = KL; s < nie; ++s) {
+                            const unsigned long long info = info_of(*spp(s, 3));
+                            if ((info >> 20) & 1) {
+                                const uint32_t ao = (uint32_t)(info >> 32) & 0xffffu, bo = (uint32_t)(info >> 48);
+                                warm_half(row(ao), row(bo), *spp(s, 0), *spp(s, 1), *spp(s, 7), dt_coef, mass(ao),
+                                          mass(bo));
+                            }
+                        }
                     }
+                    for (int itr = 0; itr < 10; ++itr) {
+                        sfor<KL>([&](auto Q) {
+                            constexpr int q = Q;
+                            if (q < m) apply_half(qra[q], qrb[q], qnx[q], qny[q], qnm[q], qc[q], qma[q], qmb[q], qacc[q]);
+                        });
+                        for (int s = KL; s < nie; ++s) {
+                            const unsigned long long info = info_of(*spp(s, 3));
+                            const uint32_t ao = (uint32_t)(info >> 32) & 0xffffu, bo = (uint32_t)(info >> 48);
+                            double* const accp = spp(s, 6 + h);
+                            double acc = *accp;
+                            apply_half(row(ao), row(bo), *spp(s, 0), *spp(s, 1), *spp(s, 2), *spp(s, 4 + h), mass(ao),
+                                       mass(bo), acc);
+                            *accp = acc;
+                        }
+                    }
+                    sfor<KL>([&](auto Q) {  // jBias / jnAcc back into the record (the arbiter cache reads jnAcc)
+                        constexpr int q = Q;
+                        if (q < m) {
+                            if (h) sh->rec[q][3][ie].y = qacc[q];
+                            else sh->rec[q][3][ie].x = qacc[q];
+                        }
+                    });
                 }
             }
-            sfor<MR>([&](auto Q) {  // jnAcc for the arbiter cache
-                constexpr int q = Q;
-                if (q < m) sh->rec[q][3][ln] = make_double2(qjn[q], qjb[q]);
-            });
-            sfor<S::Nb>([&](auto K) {
-                constexpr int k = K;
-                const double2 v = sh->v[k][ln], vb = sh->vb[k][ln];
-                e.vx[k] = v.x;
-                e.vy[k] = v.y;
-                e.bx[k] = vb.x;
-                e.by[k] = vb.y;
-            });
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (n > 0) {
+                sfor<S::Nb>([&](auto K) {
+                    constexpr int k = K;
+                    const double2 v = sh->v(k, ln), vb = sh->vb(k, ln);
+                    e.vx[k] = v.x;
+                    e.vy[k] = v.y;
+                    e.bx[k] = vb.x;
+                    e.by[k] = vb.y;
+                });
+            }
         }
     }
 
@@ -967,6 +928,8 @@ __device__ __forceinline__ void load_seg_table(const V1Params& P, Scratch<N, EPW
         g.rL2 = P.rL2[s];
         sh.seg[s] = g;
     }
+    if (s <= V1Shape<N>::Nb)  // inverse masses by solver row (Player/Ball mass, static Z)
+        sh.minv[s] = s == V1Shape<N>::Nb ? 0.0 : (s == V1Shape<N>::BALL ? kBallMinv : kPlayerMinv);
     __syncthreads();
 }
 
