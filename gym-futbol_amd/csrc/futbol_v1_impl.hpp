@@ -111,13 +111,14 @@ struct V1Shape {
 
 __device__ __forceinline__ double minv_of(int k, int ball) { return k == ball ? kBallMinv : kPlayerMinv; }
 
-// correctly rounded x / c for a constant c > 0 with rc = RN(1/c).  x = +-0 returns x * rc
-// (the correction step would turn -0 into +0)
+// correctly rounded x / c for a constant c > 0 with rc = RN(1/c).  The quotient has x's sign
+// (c > 0), which copysign restores for x = -0 (the correction step alone would give +0) -- a
+// bit operation instead of a compare and select
 __device__ __forceinline__ double cdiv(double x, double c, double rc)
 {
     const double q0 = x * rc;
     const double r = __builtin_fma(-q0, c, x);
-    return x == 0.0 ? q0 : __builtin_fma(r, rc, q0);
+    return __builtin_copysign(__builtin_fma(r, rc, q0), x);
 }
 
 struct SegLds {
@@ -144,39 +145,37 @@ struct Scratch {
     // velocities (v rows) for the per-lane dynamic body index.
     double2 rows[2 * S::Nb + 1][EPW];
     double minv[S::Nb + 1];  // inverse mass by row: players, ball, Z = 0
-    uint8_t item_env[EPW];   // split solve: compacted list of the lanes (envs) with contacts
-    uint16_t item_n[EPW];    // ... and their record counts
-    uint8_t item_pc[EPW];    // ... and the dt code of their previous cpSpaceStep (warm-start dt ratio)
+    uint8_t item_env[EPW + 1];  // split solve: compacted list of the lanes (envs) with contacts (+ a spare slot)
+    uint16_t item_n[EPW + 1];   // ... and their record counts
+    uint8_t item_pc[EPW + 1];   // ... and the dt code of their previous cpSpaceStep (warm-start dt ratio)
     SegLds seg[kNSeg];
 
     __device__ __forceinline__ double2& vb(int k, int l) { return rows[k][l]; }
     __device__ __forceinline__ double2& v(int k, int l) { return rows[2 * S::Nb - k][l]; }
 };
 
-// info word (64 bits, stored as the bits of a double):
-//   low 32: a (5 bits) | bcode (6 bits: body id, or 32 + segment) << 5 | pair << 11 | normal << 20
-//   high 32: row offset of a (k * ROW) | row offset of b (Nb * ROW = Z for segments) << 16,
-//            filled in by with_rows() in the solver prologue (not at the many collide sites:
-//            constants hoisted out of them cost registers)
+// info word (64 bits, stored as the bits of a double; only the low 32 are used):
+//   a (5 bits) | bcode (6 bits: body id, or 32 + segment) << 5 | pair << 11 | normal << 20
 __device__ __forceinline__ long long pack_info(int a, int bcode, int pair, bool normal)
 {
     return (long long)(uint32_t)(a | (bcode << 5) | (pair << 11) | ((normal ? 1 : 0) << 20));
 }
+// solver row offsets of a record's bodies: k * ROW for body k, Nb * ROW (the static row Z) for a
+// segment's static body
 template <int N, int EPW>
-__device__ __forceinline__ long long with_rows(long long info)
+__device__ __forceinline__ void info_rows(unsigned long long info, uint32_t& ao, uint32_t& bo)
 {
     constexpr uint32_t ROW = EPW * (uint32_t)sizeof(double2);
     const uint32_t lo = (uint32_t)info;
     const uint32_t a = lo & 31u, bcode = (lo >> 5) & 63u;
-    const uint32_t b = bcode < 32u ? bcode : (uint32_t)V1Shape<N>::Nb;
-    return (long long)(((unsigned long long)((a * ROW) | ((b * ROW) << 16)) << 32) | lo);
+    ao = a * ROW;
+    bo = (bcode < 32u ? bcode : (uint32_t)V1Shape<N>::Nb) * ROW;
 }
-// null record (slots between a lane's contact count and the wave's): both rows static
-template <int N, int EPW>
+// null record (slots between a lane's contact count and the wave's): both bodies static (a = Z)
+template <int N>
 __device__ __forceinline__ long long null_info()
 {
-    constexpr uint32_t R = (uint32_t)(V1Shape<N>::Nb * EPW * (int)sizeof(double2));
-    return (long long)(((unsigned long long)(R | (R << 16)) << 32));
+    return pack_info(V1Shape<N>::Nb, 32, 0, false);
 }
 
 // global spill record (slot s >= K): 8 doubles [nx, ny, nMass, info, bias, -bounce, jBias, jnAcc]
@@ -445,12 +444,12 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
     });
     // collide in canonical order; cpArbiterUpdate + preStep folded in (needs pre-damping v)
     int n = 0;
+    // nMass = 1 / (a.m_inv + b.m_inv) (cpArbiterPreStep), a compile-time constant per body pair
     auto record = [&](int a, int bcode, int pair, double nx, double ny, double p1x, double p1y, double p2x,
-                      double p2y, double apx, double apy, double avx, double avy, double ma, double bpx, double bpy,
-                      double bvx_, double bvy_, double mb, double ee) {
+                      double p2y, double apx, double apy, double avx, double avy, double bpx, double bpy,
+                      double bvx_, double bvy_, double nMass, double ee) {
         const double r1x = p1x - apx, r1y = p1y - apy;
         const double r2x = p2x - bpx, r2y = p2y - bpy;
-        const double nMass = 1.0 / (ma + mb);
         const double bdx = bpx - apx, bdy = bpy - apy;
         const double dist = ((r2x - r1x) + bdx) * nx + ((r2y - r1y) + bdy) * ny;
         double m = dist + slop;
@@ -516,12 +515,13 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
             const int i = i0 + bi;
             const double2 pi_ = sh_->vb(i, ln_), vi = sh_->v(i, ln_);
             const bool ball = i == S::BALL;
-            const double ri = ball ? kBallR : kPlayerR, mi = ball ? kBallMinv : kPlayerMinv;
+            const double ri = ball ? kBallR : kPlayerR;
+            constexpr double nmB = 1.0 / (kBallMinv + 0.0), nmP = 1.0 / (kPlayerMinv + 0.0);  // b static
             const SegLds g = sh_->seg[sg];
             double nx, ny, p1x, p1y, p2x, p2y;
             if (cs_test(pi_.x, pi_.y, ri, g, nx, ny, p1x, p1y, p2x, p2y))
-                record(i, 32 + sg, i * kNSeg + sg, nx, ny, p1x, p1y, p2x, p2y, pi_.x, pi_.y, vi.x, vi.y, mi, 0.0,
-                       0.0, 0.0, 0.0, 0.0, kE * 0.0);
+                record(i, 32 + sg, i * kNSeg + sg, nx, ny, p1x, p1y, p2x, p2y, pi_.x, pi_.y, vi.x, vi.y, 0.0, 0.0,
+                       0.0, 0.0, ball ? nmB : nmP, kE * 0.0);
         }
     });
 
@@ -541,8 +541,9 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
                 double nx, ny, p1x, p1y, p2x, p2y;
                 if (cc_test(e.px[i], e.py[i], ri, e.px[j], e.py[j], rj, nx, ny, p1x, p1y, p2x, p2y)) {
                     constexpr int pair = S::Nb * kNSeg + i * S::Nb - i * (i + 1) / 2 + (j - i - 1);
-                    record(i, j, pair, nx, ny, p1x, p1y, p2x, p2y, e.px[i], e.py[i], e.vx[i], e.vy[i], mi, e.px[j],
-                           e.py[j], e.vx[j], e.vy[j], mj, kE * kE);
+                    constexpr double nm = 1.0 / (mi + mj);
+                    record(i, j, pair, nx, ny, p1x, p1y, p2x, p2y, e.px[i], e.py[i], e.vx[i], e.vy[i], e.px[j],
+                           e.py[j], e.vx[j], e.vy[j], nm, kE * kE);
                 }
             });
             return;
@@ -566,11 +567,12 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
             hits &= hits - 1;
             const double2 pj = sh_->vb(j, ln_), vj = sh_->v(j, ln_);
             const bool ball_j = j == S::BALL;
-            const double rj = ball_j ? kBallR : kPlayerR, mj = ball_j ? kBallMinv : kPlayerMinv;
+            const double rj = ball_j ? kBallR : kPlayerR;
+            constexpr double nmB = 1.0 / (mi + kBallMinv), nmP = 1.0 / (mi + kPlayerMinv);
             double nx, ny, p1x, p1y, p2x, p2y;
             cc_contact(e.px[i], e.py[i], ri, pj.x, pj.y, rj, nx, ny, p1x, p1y, p2x, p2y);
-            record(i, j, pair0 + j, nx, ny, p1x, p1y, p2x, p2y, e.px[i], e.py[i], e.vx[i], e.vy[i], mi, pj.x, pj.y,
-                   vj.x, vj.y, mj, kE * kE);
+            record(i, j, pair0 + j, nx, ny, p1x, p1y, p2x, p2y, e.px[i], e.py[i], e.vx[i], e.vy[i], pj.x, pj.y,
+                   vj.x, vj.y, ball_j ? nmB : nmP, kE * kE);
         }
     });
 
@@ -650,34 +652,29 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
             atomicAdd(&st_stamps[(size_t)(blockIdx.x * EPW / 64) * 16 + 15], (unsigned long long)m);
 #endif
         if (m > 0) {
-            // owner lanes (envs with contacts) publish their rows, row offsets and padding
+            // every lane publishes its rows and pads its records to m (a lane without contacts
+            // writes its own, unused, column: no divergent branch), and the envs with contacts
+            // enter the compacted work list (the others write the spare slot EPW)
             const uint64_t act = __ballot(n > 0);
-            if (n > 0) {
-                sfor<S::Nb>([&](auto K) {
-                    constexpr int k = K;
-                    sh->v(k, ln) = make_double2(e.vx[k], e.vy[k]);
-                    sh->vb(k, ln) = make_double2(0.0, 0.0);
-                });
-                sh->rows[S::Nb][ln] = make_double2(0.0, 0.0);
-                for (int s = 0; s < nf; ++s) {
-                    const double2 r1 = sh->rec[s][1][ln];
-                    sh->rec[s][1][ln] = make_double2(r1.x, __longlong_as_double(with_rows<N, EPW>(__double_as_longlong(r1.y))));
-                }
-                for (int s = KL; s < n; ++s) {
-                    const double2 r1 = L.get(s, 1);
-                    L.put(s, 1, make_double2(r1.x, __longlong_as_double(with_rows<N, EPW>(__double_as_longlong(r1.y)))));
-                }
-                for (int s = nf; s < m; ++s) {
-                    sh->rec[s][0][ln] = make_double2(0.0, 0.0);
-                    sh->rec[s][1][ln] = make_double2(0.0, __longlong_as_double(null_info<N, EPW>()));
-                    sh->rec[s][2][ln] = make_double2(0.0, 0.0);
-                    sh->rec[s][3][ln] = make_double2(0.0, 0.0);
-                }
+            sfor<S::Nb>([&](auto K) {
+                constexpr int k = K;
+                sh->v(k, ln) = make_double2(e.vx[k], e.vy[k]);
+                sh->vb(k, ln) = make_double2(0.0, 0.0);
+            });
+            sh->rows[S::Nb][ln] = make_double2(0.0, 0.0);
+            for (int s = nf; s < m; ++s) {
+                sh->rec[s][0][ln] = make_double2(0.0, 0.0);
+                sh->rec[s][1][ln] = make_double2(0.0, __longlong_as_double(null_info<N>()));
+                sh->rec[s][2][ln] = make_double2(0.0, 0.0);
+                sh->rec[s][3][ln] = make_double2(0.0, 0.0);
+            }
+            {
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
-                sh->item_env[rank] = (uint8_t)ln;
-                sh->item_n[rank] = (uint16_t)n;
-                sh->item_pc[rank] = (uint8_t)pc;
+                const uint32_t slot = n > 0 ? rank : (uint32_t)EPW;
+                sh->item_env[slot] = (uint8_t)ln;
+                sh->item_n[slot] = (uint16_t)n;
+                sh->item_pc[slot] = (uint8_t)pc;
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -687,6 +684,7 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
             const int w = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
             const int items = 2 * __popcll(act);
             constexpr uint32_t ROW = EPW * (uint32_t)sizeof(double2);
+            const double coef2 = dt / P.dtv[2], coef1 = dt / P.dtv[1];  // dt / prev_dt, prev_dt != 0
             for (int i0 = 0; i0 < items; i0 += A) {
                 const int it_ = i0 + w;
                 if (it_ < items) {
@@ -695,8 +693,7 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
                     // cpArbiterApplyCachedImpulse's dt ratio of THIS env (its previous step may have
                     // been a 1e-4 reset micro-step)
                     const uint32_t ipc = sh->item_pc[it_ >> 1];
-                    const double iprev = ipc == 2 ? P.dtv[2] : (ipc == 1 ? P.dtv[1] : 0.0);
-                    const double dt_coef = (iprev == 0.0) ? 0.0 : dt / iprev;
+                    const double dt_coef = ipc == 2 ? coef2 : (ipc == 1 ? coef1 : 0.0);
                     char* const base = (char*)&sh->rows[h ? 2 * S::Nb : 0][ie];
                     const int sgn = h ? -1 : 1;
                     const double* const mtab = sh->minv;
@@ -723,7 +720,8 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
                             const double2 r0 = sh->rec[q][0][ie], r1 = sh->rec[q][1][ie], r2 = sh->rec[q][2][ie],
                                           r3 = sh->rec[q][3][ie];
                             const unsigned long long info = info_of(r1.y);
-                            const uint32_t ao = (uint32_t)(info >> 32) & 0xffffu, bo = (uint32_t)(info >> 48);
+                            uint32_t ao, bo;
+                            info_rows<N, EPW>(info, ao, bo);
                             qnx[q] = r0.x;
                             qny[q] = r0.y;
                             qnm[q] = r1.x;
@@ -745,7 +743,8 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
                         for (int s = KL; s < nie; ++s) {
                             const unsigned long long info = info_of(*spp(s, 3));
                             if ((info >> 20) & 1) {
-                                const uint32_t ao = (uint32_t)(info >> 32) & 0xffffu, bo = (uint32_t)(info >> 48);
+                                uint32_t ao, bo;
+                                info_rows<N, EPW>(info, ao, bo);
                                 warm_half(row(ao), row(bo), *spp(s, 0), *spp(s, 1), *spp(s, 7), dt_coef, mass(ao),
                                           mass(bo));
                             }
@@ -758,7 +757,8 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
                         });
                         for (int s = KL; s < nie; ++s) {
                             const unsigned long long info = info_of(*spp(s, 3));
-                            const uint32_t ao = (uint32_t)(info >> 32) & 0xffffu, bo = (uint32_t)(info >> 48);
+                            uint32_t ao, bo;
+                            info_rows<N, EPW>(info, ao, bo);
                             double* const accp = spp(s, 6 + h);
                             double acc = *accp;
                             apply_half(row(ao), row(bo), *spp(s, 0), *spp(s, 1), *spp(s, 2), *spp(s, 4 + h), mass(ao),
@@ -778,16 +778,15 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (n > 0) {
-                sfor<S::Nb>([&](auto K) {
-                    constexpr int k = K;
-                    const double2 v = sh->v(k, ln), vb = sh->vb(k, ln);
-                    e.vx[k] = v.x;
-                    e.vy[k] = v.y;
-                    e.bx[k] = vb.x;
-                    e.by[k] = vb.y;
-                });
-            }
+            // (a lane without contacts reads back the v it published and v_bias = +0)
+            sfor<S::Nb>([&](auto K) {
+                constexpr int k = K;
+                const double2 v = sh->v(k, ln), vb = sh->vb(k, ln);
+                e.vx[k] = v.x;
+                e.vy[k] = v.y;
+                e.bx[k] = vb.x;
+                e.by[k] = vb.y;
+            });
         }
     }
 

@@ -1,7 +1,7 @@
 /*
  * cdiv_check.c -- TEST INFRASTRUCTURE ONLY.  Evidence for the step kernels' division by a
  * constant (csrc/futbol_v1_impl.hpp `cdiv`): q0 = RN(x * rc), r = fma(-q0, c, x) (exact),
- * q = fma(r, rc, q0), rc = RN(1 / c), compared bit for bit with the IEEE quotient RN(x / c)
+ * q = copysign(fma(r, rc, q0), x), rc = RN(1 / c), compared bit for bit with the IEEE quotient RN(x / c)
  * that the reference (CPython float division) computes.  The GPU's v_fma_f64 / v_mul_f64 are
  * the same correctly rounded IEEE operations as C's fma() and *, so agreement here is
  * agreement there.  Samples: random doubles over a wide exponent range, plus x chosen so that
@@ -24,7 +24,7 @@ static double cdiv(double x, double c, double rc)
 {
     const double q0 = x * rc;
     const double r = fma(-q0, c, x);
-    return x == 0.0 ? q0 : fma(r, rc, q0);
+    return copysign(fma(r, rc, q0), x);
 }
 
 static int same(double a, double b)
@@ -42,6 +42,9 @@ long long orc_cdiv_check(double c, long long n, uint64_t seed, int emax)
     const double rc = 1.0 / c;
     long long bad = 0;
     uint64_t s = seed;
+    /* signed zeros: the quotient keeps x's sign */
+    if (!same(cdiv(0.0, c, rc), 0.0 / c)) ++bad;
+    if (!same(cdiv(-0.0, c, rc), -0.0 / c)) ++bad;
     for (long long k = 0; k < n; ++k) {
         /* random sign, exponent, mantissa */
         uint64_t u = sm64(&s);
