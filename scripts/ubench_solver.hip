@@ -3,7 +3,7 @@
 // records over Nb = 5 body rows + the static row, 10 sweeps.  Variants:
 //   0: the kernel's loop (rows read after the previous record's writes)
 //   1: + the v-half rows on a column swizzled by 8 (the two halves of an env on different banks)
-//   2: + next record's rows prefetched before this record's writes, forwarded by loop-invariant
+//   2: (no swizzle) next record's rows prefetched before this record's writes, forwarded by loop-invariant
 //      alias masks
 //   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -o ubench_solver scripts/ubench_solver.hip
 #include <hip/hip_runtime.h>
@@ -59,7 +59,7 @@ __global__ void __launch_bounds__(64) k_solve(const int* __restrict__ pairs, dou
     __syncthreads();
     // item: env column = partner pairs (lane 2i, 2i+1 = the two halves of env i)
     const int e = ln >> 1, h = ln & 1;
-    const int col = (VAR >= 1 && h) ? (e ^ 8) : e;
+    const int col = (VAR == 1 && h) ? (e ^ 8) : e;
     char* base = (char*)&rows[h ? 2 * NB : 0][col];
     const int sgn = h ? -1 : 1;
     double2* ra[M];
@@ -149,6 +149,19 @@ static void run(const int* d_pairs, double* out, unsigned long long* cyc, const 
            ms * 1e3);
 }
 
+static void compare(const int* d, double* o1, double* o2, unsigned long long* cyc)
+{
+    hipLaunchKernelGGL((k_solve<4, 0>), dim3(1024), dim3(64), 0, 0, d, o1, cyc);
+    hipLaunchKernelGGL((k_solve<4, 2>), dim3(1024), dim3(64), 0, 0, d, o2, cyc);
+    CHECK(hipDeviceSynchronize());
+    static double h1[1024 * 64], h2[1024 * 64];
+    CHECK(hipMemcpy(h1, o1, sizeof(h1), hipMemcpyDeviceToHost));
+    CHECK(hipMemcpy(h2, o2, sizeof(h2), hipMemcpyDeviceToHost));
+    int bad = 0;
+    for (int i = 0; i < 1024 * 64; ++i) bad += h1[i] != h2[i];
+    printf("variant 0 vs 2 (M=4) differing lanes: %d\n", bad);
+}
+
 int main()
 {
     // random records: a in 0..4, b in {0..4} \ {a} or static (NB), as in a crowded env
@@ -171,11 +184,14 @@ int main()
     CHECK(hipMalloc(&out, 1024 * 64 * sizeof(double)));
     CHECK(hipMalloc(&cyc, 8));
     CHECK(hipMemcpy(d, h, n * sizeof(int), hipMemcpyHostToDevice));
+    double* out2;
+    CHECK(hipMalloc(&out2, 1024 * 64 * sizeof(double)));
+    compare(d, out, out2, cyc);
     run<4, 0>(d, out, cyc, "kernel loop");
     run<4, 1>(d, out, cyc, "v rows swizzled");
-    run<4, 2>(d, out, cyc, "swizzled + prefetch/forward");
+    run<4, 2>(d, out, cyc, "prefetch/forward");
     run<8, 0>(d, out, cyc, "kernel loop");
     run<8, 1>(d, out, cyc, "v rows swizzled");
-    run<8, 2>(d, out, cyc, "swizzled + prefetch/forward");
+    run<8, 2>(d, out, cyc, "prefetch/forward");
     return 0;
 }
