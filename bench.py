@@ -7,7 +7,9 @@
 Workload (BASELINE.json configs[1]/[3]): B = 65 536 independent 2v2 envs_v1
 matches per GPU, synthetic random left-team actions (Philox, generated on the
 GPU by fill_actions), opponent random actions drawn inside the step kernel,
-DummyVecEnv auto-reset; every step writes obs/reward/done to HBM.  A "step" =
+DummyVecEnv auto-reset; every step writes obs/reward/done to HBM.  (Staggered
+episode phases would be --stagger 1; by default all envs run in lockstep, as DummyVecEnv
+runs them, and a timed region shorter than an episode sits mid-episode).  A "step" =
 fill_actions + one env-step launch over all B envs.  N > 1: one process per
 GPU, env shards with global env ids rank*B..; weak scaling; one RCCL
 all_reduce(SUM) of [episode-return sum, episodes, env-steps] every 300 steps
@@ -150,6 +152,9 @@ def main():
     ap.add_argument("--groups", type=int, default=1,
                     help="step the B envs as this many independent env groups (B/groups envs each: one "
                          "context, HIP stream and hipGraph per group) that advance asynchronously")
+    ap.add_argument("--stagger", type=int, default=0,
+                    help="1: spread the envs' episode starts over an episode (slower: every wave then mixes "
+                         "contact-heavy and formation phases); 0: all envs in lockstep as DummyVecEnv runs them")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=600,
                     help="steps timed per-kernel with HIP events (a multiple of the episode length)")
@@ -178,6 +183,23 @@ def main():
         venv.random_actions(ALL, seed=1234, out=act)
         venv.step_raw(act)
 
+    def stagger(ve, base):
+        """Untimed pre-roll to the steady state of a long-running vector env: the episodes of
+        the B envs start at spread-out steps (env with global id g starts at pre-roll step
+        (g * 131) mod L, L = the episode length), so any window of steps -- the driver's short
+        K as well as whole episodes -- sees every episode phase in the same proportion instead
+        of all envs in formation at once.  Same per-env dynamics; only the reset times move."""
+        L = ve.episode_steps
+        gid = torch.arange(ve.num_envs, device=dev, dtype=torch.int64) + base
+        phase = (gid * 131) % L
+        a = ve._act
+        for t in range(L):
+            ve.reset((phase == t).to(torch.uint8))
+            ve.random_actions(ALL, seed=1234, out=a)
+            ve.step_raw(a)
+
+    if args.stagger:
+        stagger(venv, R.shard(B))
     for _ in range(args.warmup):
         one_step()
     torch.cuda.synchronize(dev)
@@ -239,27 +261,59 @@ def main():
     streams = [torch.cuda.Stream(dev) for _ in groups]
 
     graphs = None
-    G = 100
+    # graphs of Gs steps each (+ the remainder as a second graph), so that short timed regions
+    # (the driver's K = 20) are replayed from a graph too rather than launched step by step
+    Gs = min(100, args.steps)
+    Gr = args.steps % Gs
+
+    def capture(ge, s, nsteps):
+        abuf = torch.empty((nsteps, ge.num_envs, ge.action_dim), dtype=torch.uint8, device=dev)
+        g_ = torch.cuda.CUDAGraph()
+        s.wait_stream(stream)
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g_, stream=s):
+                ge.random_actions_steps(nsteps, ALL, seed=1234, out=abuf)
+                for t in range(nsteps):
+                    ge.step_raw(abuf[t])
+        stream.wait_stream(s)
+        return g_, abuf
+
     if args.graph:
         graphs = []
         for ge, s in zip(groups, streams):
-            abuf = torch.empty((G, ge.num_envs, ge.action_dim), dtype=torch.uint8, device=dev)
             if ge is not venv:  # warm the group up like the main context
-                for _ in range(args.warmup):
+                if args.stagger:
+                    stagger(ge, R.shard(B) + groups.index(ge) * (B // ngroups))
+                for _ in range(args.warmup + 2 * args.profile_steps):
                     ge.random_actions(ALL, seed=1234, out=ge._act)
                     ge.step_raw(ge._act)
-            g_ = torch.cuda.CUDAGraph()
-            s.wait_stream(stream)
+            graphs.append((capture(ge, s, Gs), capture(ge, s, Gr) if Gr else None))
+        # one untimed replay of each graph: the first launch of a graph pays its upload
+        for (gm, gr), s in zip(graphs, streams):
             with torch.cuda.stream(s):
-                with torch.cuda.graph(g_, stream=s):
-                    ge.random_actions_steps(G, ALL, seed=1234, out=abuf)
-                    for t in range(G):
-                        ge.step_raw(abuf[t])
-            stream.wait_stream(s)
-            graphs.append((g_, abuf))
+                gm[0].replay()
+                if gr:
+                    gr[0].replay()
         torch.cuda.synchronize(dev)
     elif ngroups > 1:
         raise SystemExit("--groups needs --graph 1")
+
+    # all envs run their fixed-length episodes in lockstep (DummyVecEnv: one reset at the
+    # start, auto-reset every L steps), and a step's cost depends on the episode phase (the
+    # first ~75 steps from formation are cheap).  A timed region shorter than an episode is
+    # placed in the middle of one by untimed steps, so that it does not sit on the cheap start;
+    # K a multiple of L measures whole episodes exactly.
+    L = venv.episode_steps
+    align = 0
+    if not args.stagger and args.steps < L:
+        at = (args.warmup + 2 * args.profile_steps + (Gs + Gr if graphs is not None else 0)) % L  # every env's step
+        align = ((L - args.steps) // 2 - at) % L
+        for ge, s in zip(groups, streams):
+            with torch.cuda.stream(s):
+                for _ in range(align):
+                    ge.random_actions(ALL, seed=1234, out=ge._act)
+                    ge.step_raw(ge._act)
+            stream.wait_stream(s)
 
     def all_stats():
         tot = torch.zeros(3, dtype=torch.float64, device=dev)
@@ -275,11 +329,11 @@ def main():
     t0 = time.perf_counter()
     done_steps = 0
     while done_steps < args.steps:
-        chunk = min(G, args.steps - done_steps) if graphs is not None else 1
-        if graphs is not None and chunk == G:
-            for (g_, _), s in zip(graphs, streams):
+        chunk = (Gs if args.steps - done_steps >= Gs else Gr) if graphs is not None else 1
+        if graphs is not None:
+            for (gm, gr), s in zip(graphs, streams):
                 with torch.cuda.stream(s):
-                    g_.replay()
+                    (gm if chunk == Gs else gr)[0].replay()
         elif ngroups > 1:
             for ge, s in zip(groups, streams):
                 with torch.cuda.stream(s):
@@ -314,6 +368,10 @@ def main():
         "config": {"workload": ("C2/C4: %d envs/GPU envs_v1 %dv%d, synthetic random actions, auto-reset"
                                 % (B, n, n)) if args.kind == "v1" else
                    ("C3: %d envs/GPU v0 FutbolEnv, hard-coded opponent" % B),
+                   "episode_phases": "staggered" if args.stagger else "lockstep (DummyVecEnv)",
+                   "timed_from_episode_step": None if args.stagger else
+                   (args.warmup + 2 * args.profile_steps + (Gs + Gr if graphs is not None else 0) + align)
+                   % venv.episode_steps,
                    "envs_per_gpu": B, "global_envs": B * world, "parallelism": "dp%d" % world,
                    "obs_dtype": "f32", "hip_graph": bool(graphs is not None), "env_groups": ngroups},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

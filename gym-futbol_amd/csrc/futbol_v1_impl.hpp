@@ -43,13 +43,14 @@ constexpr double kPlayerR = 1.5, kBallR = 1.0, kSegR = 1.0;
 constexpr double kPlayerMinv = 1.0 / 20.0, kBallMinv = 1.0 / 10.0;
 constexpr double kPlayerVmax = 10.0, kBallVmax = 25.0;
 constexpr double kE = 0.2;  // elasticity of players and ball; segments 0
-// arbiter-cache entries preloaded into registers (5v5 / 10v10 envs hold more cached arbiters:
-// a lane with more than CK entries sends its whole wave through the global lookup loops)
-#ifndef FUTBOL_CK5
-#define FUTBOL_CK5 8
+// arbiter-cache entries preloaded into registers: 4 for N < 5, FUTBOL_CK_LARGE (8) for every
+// N >= 5 (5v5 and 10v10 envs hold more cached arbiters: a lane with more than CKN entries sends
+// its whole wave through the global lookup loops)
+#ifndef FUTBOL_CK_LARGE
+#define FUTBOL_CK_LARGE 8
 #endif
 template <int N>
-constexpr int CKN = N >= 5 ? FUTBOL_CK5 : 4;
+constexpr int CKN = N >= 5 ? FUTBOL_CK_LARGE : 4;
 // entries beyond CKN read per batch of independent loads (5v5 and up: registers are exhausted)
 template <int N>
 constexpr int CBN = N >= 5 ? 1 : 4;
@@ -1209,7 +1210,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
             position_to_initial<N>(P, e);
         }
         FUTBOL_STAMP(ph == 0 ? 3 : 9);
-        if (ph != 0) load_cache_pre<N, EPW>(L, e.meta.ncache(), ck, cj);  // the cache phase 0 left behind
+        if (ph != 0) load_cache_pre<N, EPW>(L, e.meta.ncache(), ck, cj);  // the cache the previous phase left behind
         space_step<N, EPW>(P, L, e, ph == 0 ? 2 : 1, ck, cj
 #ifdef FUTBOL_STAMPS
                       , st_stamps, _stamp_prev
