@@ -86,8 +86,11 @@ def pmc_traffic(kind, n, B):
 
 
 STAMP_SLOTS = ["load state", "actions + opponent RNG", "process_action + out-of-bounds", "phase glue",
-               "integrate p + collide", "cache lookups + integrate v", "warm start + 10 solver iterations",
+               "collide: circle pairs", "cache lookups + integrate v", "solve: items, warm start, 10 sweeps",
                "arbiter cache update", "reward / goal / time", "goal reset + auto-reset phases", "obs + store"]
+STAMP_STRIDE = 32  # u64 slots per wave (futbol_kernels.hpp kStampStride)
+SUB_SLOTS = {16: "integrate p", 17: "collide: stage rows + segment candidate masks", 18: "collide: segment contacts",
+             19: "solve: publish rows / records / work list"}
 
 
 def stamps_report(venv, one_step, args):
@@ -95,7 +98,7 @@ def stamps_report(venv, one_step, args):
     import ctypes as C
     from gym_futbol_amd import _native as nat
     nblk = (venv.num_envs + 63) // 64
-    buf = np.zeros((nblk + 1) * 16, np.uint64)
+    buf = np.zeros((nblk + 1) * STAMP_STRIDE, np.uint64)
     nat.check(nat.load().futbol_debug_stamps(venv.ctx.h, buf.ctypes.data, buf.size, 1), venv.ctx.h)
     steps = args.steps
     t0 = time.perf_counter()
@@ -105,15 +108,17 @@ def stamps_report(venv, one_step, args):
     wall = time.perf_counter() - t0
     nat.check(nat.load().futbol_debug_stamps(venv.ctx.h, buf.ctypes.data, buf.size, 0), venv.ctx.h)
     epw = 64
-    per = buf[:nblk * 16].reshape(nblk, 16).astype(np.float64).sum(0) / (nblk * steps * (64 // epw))  # per wave
-    tot = per[:11].sum()
+    per = buf[:nblk * STAMP_STRIDE].reshape(nblk, STAMP_STRIDE).astype(np.float64).sum(0) / (nblk * steps * (64 // epw))
+    tot = per[:11].sum() + sum(per[k] for k in SUB_SLOTS)
     rep = {"diagnostic": "stamps", "envs_per_wave": epw, "steps": steps, "ms_per_step_wall": wall / steps * 1e3,
            "cycles_per_wave_step_total": tot,
-           "phases": {STAMP_SLOTS[i]: {"cycles": per[i], "share": per[i] / tot} for i in range(11)},
-           "solver_records_per_wave_step": per[15]}
+           "phases": dict([(STAMP_SLOTS[i], {"cycles": per[i], "share": per[i] / tot}) for i in range(11)] +
+                          [(SUB_SLOTS[k], {"cycles": per[k], "share": per[k] / tot}) for k in SUB_SLOTS]),
+           "solver_records_per_wave_step": per[15],
+           "segment_candidate_iterations_per_wave_step": per[24], "segment_contact_iterations_per_wave_step": per[25]}
     # single-launch snapshots: wave start/end (100 MHz realtime), cycles, placement
     snaps = []
-    slow = np.zeros(16)
+    slow = np.zeros(STAMP_STRIDE)
     for k in range(args.snapshots):
         for _ in range(args.snapshot_stride - 1):
             one_step()
@@ -121,7 +126,7 @@ def stamps_report(venv, one_step, args):
         one_step()
         torch.cuda.synchronize()
         nat.check(nat.load().futbol_debug_stamps(venv.ctx.h, buf.ctypes.data, buf.size, 0), venv.ctx.h)
-        w = buf[:nblk * 16].reshape(nblk, 16)
+        w = buf[:nblk * STAMP_STRIDE].reshape(nblk, STAMP_STRIDE)
         slow += w[int(np.argmax(w[:, 13]))].astype(np.float64)   # phases of this launch's slowest wave
         t0_, t1_, cyc, hw = (w[:, 11].astype(np.float64), w[:, 12].astype(np.float64),
                              w[:, 13].astype(np.float64), w[:, 14])
@@ -132,7 +137,8 @@ def stamps_report(venv, one_step, args):
                       "wave_us_mean": dur.mean(), "wave_us_p90": float(np.percentile(dur, 90)), "wave_us_max": dur.max(),
                       "wave_cycles_mean": cyc.mean(), "wave_cycles_max": cyc.max(),
                       "simds_used": int(len(per_simd)), "max_waves_per_simd": int(per_simd.max())})
-    rep["slowest_wave_phases"] = {STAMP_SLOTS[i]: slow[i] / max(len(snaps), 1) for i in range(11)}
+    rep["slowest_wave_phases"] = dict([(STAMP_SLOTS[i], slow[i] / max(len(snaps), 1)) for i in range(11)] +
+                                      [(SUB_SLOTS[k], slow[k] / max(len(snaps), 1)) for k in SUB_SLOTS])
     rep["slowest_wave_records"] = slow[15] / max(len(snaps), 1)
     rep["snapshots"] = snaps
     rep["snapshot_mean"] = {k: float(np.mean([x[k] for x in snaps])) for k in snaps[0]} if snaps else None

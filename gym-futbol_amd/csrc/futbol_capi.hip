@@ -310,17 +310,17 @@ extern "C" int futbol_create(const FutbolConfig* cfg, int32_t device, uint64_t s
         s.invalid = ctx->d_invalid;
         s.stamps = nullptr;
 #ifdef FUTBOL_STAMPS
-        if ((he = hipMalloc((void**)&ctx->d_stamps, (size_t)((B + 63) / 64 + 1) * 16 * 8)) != hipSuccess)
+        if ((he = hipMalloc((void**)&ctx->d_stamps, (size_t)((B + 63) / 64 + 1) * kStampStride * 8)) != hipSuccess)
             return bail(he, "hipMalloc(stamps)");
-        if ((he = hipMemset(ctx->d_stamps, 0, (size_t)((B + 63) / 64) * 16 * 8)) != hipSuccess)
+        if ((he = hipMemset(ctx->d_stamps, 0, (size_t)((B + 63) / 64) * kStampStride * 8)) != hipSuccess)
             return bail(he, "hipMemset(stamps)");
         s.stamps = ctx->d_stamps;
 #endif
 #ifdef FUTBOL_CRUMBS
-        if ((he = hipHostMalloc((void**)&ctx->d_stamps, (size_t)((B + 63) / 64 + 1) * 16 * 8,
+        if ((he = hipHostMalloc((void**)&ctx->d_stamps, (size_t)((B + 63) / 64 + 1) * kStampStride * 8,
                                 hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
             return bail(he, "hipHostMalloc(crumbs)");
-        memset(ctx->d_stamps, 0, (size_t)((B + 63) / 64 + 1) * 16 * 8);
+        memset(ctx->d_stamps, 0, (size_t)((B + 63) / 64 + 1) * kStampStride * 8);
         s.stamps = ctx->d_stamps;
 #endif
         int rc = launch_v1(N, ctx->epw, ctx->v1_def, (const V1Params*)ctx->d_params, B, s, 0, 1, nullptr, nullptr, nullptr,
@@ -559,7 +559,7 @@ extern "C" int futbol_debug_stamps(FutbolCtx* ctx, uint64_t* host_out, int64_t n
 {
     if (!ctx || !host_out) return FUTBOL_EINVAL;
     if (!ctx->d_stamps) return fail(ctx, FUTBOL_EUNSUPPORTED, "not a FUTBOL_STAMPS diagnostic build / not v1");
-    const size_t bytes = (size_t)((ctx->B + 63) / 64) * 16 * 8;
+    const size_t bytes = (size_t)((ctx->B + 63) / 64) * kStampStride * 8;
     if ((size_t)n * 8 < bytes) return fail(ctx, FUTBOL_EINVAL, "stamps buffer too small");
 #ifdef FUTBOL_CRUMBS
     memcpy(host_out, ctx->d_stamps, bytes);  // host memory: readable even after a device fault

@@ -9,6 +9,9 @@
 
 namespace futbol {
 
+// diagnostic stamps buffer (FUTBOL_STAMPS builds): u64 slots per one-wave block
+constexpr int kStampStride = 32;
+
 // The 16 distinct bounds of the 12 segment cpBBs (taken from sl/sb/sr/st): the
 // circle-vs-segment-BB test of segment s is  cl <= r_s && l_s <= cr && cb <= t_s && b_s <= ct.
 struct BBT {

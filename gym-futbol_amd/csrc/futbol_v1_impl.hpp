@@ -56,7 +56,8 @@ template <int N>
 constexpr int CBN = N >= 5 ? 1 : 4;
 
 // Diagnostic build only (-DFUTBOL_STAMPS, bench.py --stamps): per-wave s_memtime at phase
-// boundaries, accumulated into st.stamps[wave][slot].  Never compiled into the product.
+// boundaries, accumulated into st.stamps[wave][slot] (kStampStride slots per wave: 0-10 phases,
+// 11-14 the launch snapshot, 15 solver records, 16-23 sub-phases).  Never compiled into the product.
 #ifdef FUTBOL_STAMPS
 #define FUTBOL_STAMP(slot)                                                                                \
     do {                                                                                                  \
@@ -64,7 +65,7 @@ constexpr int CBN = N >= 5 ? 1 : 4;
         const unsigned long long _t = __builtin_amdgcn_s_memtime();                                      \
         __builtin_amdgcn_s_waitcnt(0);                                                                    \
         if ((threadIdx.x & 63) == 0 && st_stamps) {                                                       \
-            atomicAdd(&st_stamps[(size_t)(blockIdx.x * EPW / 64) * 16 + (slot)], _t - _stamp_prev);                            \
+            atomicAdd(&st_stamps[(size_t)(blockIdx.x * EPW / 64) * kStampStride + (slot)], _t - _stamp_prev);                            \
         }                                                                                                 \
         _stamp_prev = _t;                                                                                 \
     } while (0)
@@ -222,10 +223,23 @@ struct Lane {
     __device__ __forceinline__ void set_rec(int s, double nx, double ny, double nm, double bi, double bo, double j,
                                             long long info) const
     {
-        put(s, 0, make_double2(nx, ny));
-        put(s, 1, make_double2(nm, __longlong_as_double(info)));
-        put(s, 2, make_double2(bi, -bo));
-        put(s, 3, make_double2(0.0, j));
+        const double2 r0 = make_double2(nx, ny), r1 = make_double2(nm, __longlong_as_double(info)),
+                      r2 = make_double2(bi, -bo), r3 = make_double2(0.0, j);
+        if (s < KL) {  // one branch for the four fields
+            sh->rec[s][0][lane] = r0;
+            sh->rec[s][1][lane] = r1;
+            sh->rec[s][2][lane] = r2;
+            sh->rec[s][3][lane] = r3;
+        } else {
+            *sp(s, 0) = r0.x;
+            *sp(s, 1) = r0.y;
+            *sp(s, 2) = r1.x;
+            *sp(s, 3) = r1.y;
+            *sp(s, 4) = r2.x;
+            *sp(s, 5) = r2.y;
+            *sp(s, 6) = r3.x;
+            *sp(s, 7) = r3.y;
+        }
     }
 };
 
@@ -336,16 +350,14 @@ __device__ __forceinline__ void seg_closest(double cx, double cy, double sax, do
     qy = say + sdy * t;
 }
 
-__device__ __forceinline__ bool cs_test(double cx, double cy, double rc, const SegLds& g, double& nx, double& ny,
-                                        double& p1x, double& p1y, double& p2x, double& p2y)
+// CircleToSegment's contact for a pair already known to collide (the same closest point and d2)
+__device__ __forceinline__ void cs_contact(double cx, double cy, double rc, const SegLds& g, double& nx, double& ny,
+                                           double& p1x, double& p1y, double& p2x, double& p2y)
 {
     double qx, qy;
     seg_closest(cx, cy, g.ax, g.ay, g.sdx, g.sdy, g.L2, g.rL2, qx, qy);
-    const double mind = rc + kSegR;
     const double dx = qx - cx, dy = qy - cy;
-    const double d2 = dx * dx + dy * dy;
-    if (!(d2 < mind * mind)) return false;
-    const double d = sqrt(d2);
+    const double d = sqrt(dx * dx + dy * dy);
     if (d != 0.0) {
         const double inv = 1.0 / d;
         nx = dx * inv;
@@ -359,7 +371,6 @@ __device__ __forceinline__ bool cs_test(double cx, double cy, double rc, const S
     p1y = cy + ny * rc;
     p2x = qx + nx * (-kSegR);
     p2y = qy + ny * (-kSegR);
-    return true;
 }
 
 __device__ __forceinline__ bool cs_hit(const V1Params& P, int s, double cx, double cy, double rc)
@@ -431,6 +442,7 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
     });
 
     FUTBOL_CRUMB(L, 10 + dtc);
+    FUTBOL_STAMP(dtc == 2 ? 16 : 9);
     // bodies' positions (v_bias rows) and velocities (v rows) staged in LDS for the per-lane
     // dynamic body index of the contact loops; the solver prologue overwrites both
     // (5v5: +6% step throughput; 2v2: -3% -- the staging and the bit loops cost more than the
@@ -476,6 +488,7 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
     // word); one contact test per set bit, so a wave runs max-over-lanes(candidates of the word)
     // iterations rather than one loop per body that any lane needs.  The body is indexed
     // dynamically through the LDS rows staged above.
+    FUTBOL_STAMP(dtc == 2 ? 17 : 9);
     constexpr int BPW = 5;
     constexpr int NWS = (S::Nb + BPW - 1) / BPW;
     sfor<NWS>([&](auto WD) {
@@ -508,9 +521,44 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
             c |= (rW3 && lW1 && thi && bhi) ? 1u << 11 : 0u;
             cand |= interior ? 0ull : (uint64_t)c << (kNSeg * (i - i0));
         });
+        // two passes: the exact hit test of every candidate (branch-free, into a hit mask), then
+        // the contact and record of every hit -- a wave runs the expensive contact path
+        // max-over-lanes(hits) times rather than once per candidate iteration in which any lane hits
+        uint64_t hitm = 0;
+#ifdef FUTBOL_STAMPS
+        {   // diagnostic: the wave's candidate iterations (max over lanes of the candidate count)
+            int c = __popcll(cand);
+            for (int o = 32; o >= 1; o >>= 1) { const int t = __shfl_xor(c, o); c = t > c ? t : c; }
+            if ((threadIdx.x & 63) == 0 && st_stamps && dtc == 2)
+                atomicAdd(&st_stamps[(size_t)(blockIdx.x * EPW / 64) * kStampStride + 24], (unsigned long long)c);
+        }
+#endif
         while (cand) {
             const int bit = __builtin_ctzll(cand);
             cand &= cand - 1;
+            const int bi = bit / kNSeg;
+            const int sg = bit - bi * kNSeg;
+            const int i = i0 + bi;
+            const double2 pi_ = sh_->vb(i, ln_);
+            const double ri = i == S::BALL ? kBallR : kPlayerR;
+            const SegLds g = sh_->seg[sg];
+            double qx, qy;
+            seg_closest(pi_.x, pi_.y, g.ax, g.ay, g.sdx, g.sdy, g.L2, g.rL2, qx, qy);
+            const double mind = ri + kSegR;
+            const double dx = qx - pi_.x, dy = qy - pi_.y;
+            hitm |= (dx * dx + dy * dy < mind * mind) ? 1ull << bit : 0ull;
+        }
+#ifdef FUTBOL_STAMPS
+        {   // diagnostic: the wave's contact iterations (max over lanes of the hit count)
+            int c = __popcll(hitm);
+            for (int o = 32; o >= 1; o >>= 1) { const int t = __shfl_xor(c, o); c = t > c ? t : c; }
+            if ((threadIdx.x & 63) == 0 && st_stamps && dtc == 2)
+                atomicAdd(&st_stamps[(size_t)(blockIdx.x * EPW / 64) * kStampStride + 25], (unsigned long long)c);
+        }
+#endif
+        while (hitm) {
+            const int bit = __builtin_ctzll(hitm);
+            hitm &= hitm - 1;
             const int bi = bit / kNSeg;
             const int sg = bit - bi * kNSeg;
             const int i = i0 + bi;
@@ -520,12 +568,13 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
             constexpr double nmB = 1.0 / (kBallMinv + 0.0), nmP = 1.0 / (kPlayerMinv + 0.0);  // b static
             const SegLds g = sh_->seg[sg];
             double nx, ny, p1x, p1y, p2x, p2y;
-            if (cs_test(pi_.x, pi_.y, ri, g, nx, ny, p1x, p1y, p2x, p2y))
-                record(i, 32 + sg, i * kNSeg + sg, nx, ny, p1x, p1y, p2x, p2y, pi_.x, pi_.y, vi.x, vi.y, 0.0, 0.0,
-                       0.0, 0.0, ball ? nmB : nmP, kE * 0.0);
+            cs_contact(pi_.x, pi_.y, ri, g, nx, ny, p1x, p1y, p2x, p2y);
+            record(i, 32 + sg, i * kNSeg + sg, nx, ny, p1x, p1y, p2x, p2y, pi_.x, pi_.y, vi.x, vi.y, 0.0, 0.0,
+                   0.0, 0.0, ball ? nmB : nmP, kE * 0.0);
         }
     });
 
+    FUTBOL_STAMP(dtc == 2 ? 18 : 9);
     // (2) circle-circle contacts, pairs (i, j > i) in row-major order
     sfor<S::Nb>([&](auto I) {
         constexpr int i = I;
@@ -650,7 +699,7 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
         const bool spill = __ballot(n > KL) != 0;
 #ifdef FUTBOL_STAMPS
         if ((threadIdx.x & 63) == 0 && st_stamps && dtc == 2)
-            atomicAdd(&st_stamps[(size_t)(blockIdx.x * EPW / 64) * 16 + 15], (unsigned long long)m);
+            atomicAdd(&st_stamps[(size_t)(blockIdx.x * EPW / 64) * kStampStride + 15], (unsigned long long)m);
 #endif
         if (m > 0) {
             // every lane publishes its rows and pads its records to m (a lane without contacts
@@ -680,6 +729,7 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            FUTBOL_STAMP(dtc == 2 ? 19 : 9);
             const uint64_t live = __ballot(1);
             const int A = __popcll(live);
             const int w = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
@@ -1271,7 +1321,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
     // snapshot of THIS launch (overwritten every launch): start / end realtime (100 MHz),
     // wave cycles, and where the wave ran (HW_ID: wave, simd, cu, sh, se | XCC_ID << 32)
     if ((threadIdx.x & 63) == 0 && st_stamps) {
-        unsigned long long* w = &st_stamps[(size_t)(blockIdx.x * EPW / 64) * 16];
+        unsigned long long* w = &st_stamps[(size_t)(blockIdx.x * EPW / 64) * kStampStride];
         const unsigned long long real1 = __builtin_amdgcn_s_memrealtime();
         const unsigned long long cyc1 = __builtin_amdgcn_s_memtime();
         const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
