@@ -86,10 +86,10 @@ def pmc_traffic(kind, n, B):
 
 
 STAMP_SLOTS = ["load state", "actions + opponent RNG", "process_action + out-of-bounds", "phase glue",
-               "collide: circle pairs", "cache lookups + integrate v", "solve: items, warm start, 10 sweeps",
+               "collide: contacts + records (work list)", "cache lookups + integrate v", "solve: items, warm start, 10 sweeps",
                "arbiter cache update", "reward / goal / time", "goal reset + auto-reset phases", "obs + store"]
 STAMP_STRIDE = 32  # u64 slots per wave (futbol_kernels.hpp kStampStride)
-SUB_SLOTS = {16: "integrate p", 17: "collide: stage rows + segment candidate masks", 18: "collide: segment contacts",
+SUB_SLOTS = {16: "integrate p", 17: "collide: stage rows", 18: "collide: hit tests (segments, pairs)",
              19: "solve: publish rows / records / work list"}
 
 

@@ -443,11 +443,8 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
 
     FUTBOL_CRUMB(L, 10 + dtc);
     FUTBOL_STAMP(dtc == 2 ? 16 : 9);
-    // bodies' positions (v_bias rows) and velocities (v rows) staged in LDS for the per-lane
-    // dynamic body index of the contact loops; the solver prologue overwrites both
-    // (5v5: +6% step throughput; 2v2: -3% -- the staging and the bit loops cost more than the
-    // 10 pair branches they replace, so few-body instances keep the branches)
-    constexpr bool kCompactPairs = N >= 5;
+    // bodies' positions (v_bias rows) and velocities (v rows) staged in LDS for the dynamic body
+    // (and env column) indices of the contact work list; the solver prologue overwrites both
     Scratch<N, EPW>* const sh_ = L.sh;
     const int ln_ = L.lane;
     sfor<S::Nb>([&](auto K) {
@@ -457,40 +454,15 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
     });
     // collide in canonical order; cpArbiterUpdate + preStep folded in (needs pre-damping v)
     int n = 0;
-    // nMass = 1 / (a.m_inv + b.m_inv) (cpArbiterPreStep), a compile-time constant per body pair
-    auto record = [&](int a, int bcode, int pair, double nx, double ny, double p1x, double p1y, double p2x,
-                      double p2y, double apx, double apy, double avx, double avy, double bpx, double bpy,
-                      double bvx_, double bvy_, double nMass, double ee) {
-        const double r1x = p1x - apx, r1y = p1y - apy;
-        const double r2x = p2x - bpx, r2y = p2y - bpy;
-        const double bdx = bpx - apx, bdy = bpy - apy;
-        const double dist = ((r2x - r1x) + bdx) * nx + ((r2y - r1y) + bdy) * ny;
-        double m = dist + slop;
-        m = (0.0 < m) ? 0.0 : m;
-        const double bias = cdiv(-biasCoef * m, dt, rdt);
-        const double bounce = ((bvx_ - avx) * nx + (bvy_ - avy) * ny) * ee;
-        double jn = 0.0;
-        bool normal = false;
-#pragma unroll
-        for (int c = 0; c < CKN<N>; ++c)
-            if ((int)(ck[c] & 0x3ffu) == pair) {
-                jn = cj[c];
-                normal = (ck[c] >> 12) == 0;  // touched by the previous step: NORMAL -> warm start
-                touched |= 1u << c;
-            }
-        FB_BOUND(L, n < S::P && pair < S::P, 5, n = S::P - 1);
-        L.set_rec(n, nx, ny, nMass, bias, bounce, jn, pack_info(a, bcode, pair, normal));
-        ++n;
-    };
-
-    // (1) circle-segment contacts of all bodies, (body, segment) ascending: cpBBIntersects from
-    // the 16 distinct segment bounds as a 12-bit field per body in 60-bit words (5 bodies per
-    // word); one contact test per set bit, so a wave runs max-over-lanes(candidates of the word)
-    // iterations rather than one loop per body that any lane needs.  The body is indexed
-    // dynamically through the LDS rows staged above.
+    constexpr int KLs = Lane<N, EPW>::KL;
+    // (1) circle-segment hits of all bodies, (body, segment) ascending: cpBBIntersects from the
+    // 16 distinct segment bounds as a 12-bit field per body in 60-bit words (5 bodies per word),
+    // then the exact CircleToSegment test of every candidate bit (the body indexed dynamically
+    // through the LDS rows staged above) into a hit word per 5 bodies
     FUTBOL_STAMP(dtc == 2 ? 17 : 9);
     constexpr int BPW = 5;
     constexpr int NWS = (S::Nb + BPW - 1) / BPW;
+    uint64_t hsw[NWS];
     sfor<NWS>([&](auto WD) {
         constexpr int w = WD;
         constexpr int i0 = w * BPW, i1 = (w + 1) * BPW < S::Nb ? (w + 1) * BPW : S::Nb;
@@ -521,18 +493,7 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
             c |= (rW3 && lW1 && thi && bhi) ? 1u << 11 : 0u;
             cand |= interior ? 0ull : (uint64_t)c << (kNSeg * (i - i0));
         });
-        // two passes: the exact hit test of every candidate (branch-free, into a hit mask), then
-        // the contact and record of every hit -- a wave runs the expensive contact path
-        // max-over-lanes(hits) times rather than once per candidate iteration in which any lane hits
         uint64_t hitm = 0;
-#ifdef FUTBOL_STAMPS
-        {   // diagnostic: the wave's candidate iterations (max over lanes of the candidate count)
-            int c = __popcll(cand);
-            for (int o = 32; o >= 1; o >>= 1) { const int t = __shfl_xor(c, o); c = t > c ? t : c; }
-            if ((threadIdx.x & 63) == 0 && st_stamps && dtc == 2)
-                atomicAdd(&st_stamps[(size_t)(blockIdx.x * EPW / 64) * kStampStride + 24], (unsigned long long)c);
-        }
-#endif
         while (cand) {
             const int bit = __builtin_ctzll(cand);
             cand &= cand - 1;
@@ -548,83 +509,206 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
             const double dx = qx - pi_.x, dy = qy - pi_.y;
             hitm |= (dx * dx + dy * dy < mind * mind) ? 1ull << bit : 0ull;
         }
-#ifdef FUTBOL_STAMPS
-        {   // diagnostic: the wave's contact iterations (max over lanes of the hit count)
-            int c = __popcll(hitm);
-            for (int o = 32; o >= 1; o >>= 1) { const int t = __shfl_xor(c, o); c = t > c ? t : c; }
-            if ((threadIdx.x & 63) == 0 && st_stamps && dtc == 2)
-                atomicAdd(&st_stamps[(size_t)(blockIdx.x * EPW / 64) * kStampStride + 25], (unsigned long long)c);
-        }
-#endif
-        while (hitm) {
-            const int bit = __builtin_ctzll(hitm);
-            hitm &= hitm - 1;
-            const int bi = bit / kNSeg;
-            const int sg = bit - bi * kNSeg;
-            const int i = i0 + bi;
-            const double2 pi_ = sh_->vb(i, ln_), vi = sh_->v(i, ln_);
-            const bool ball = i == S::BALL;
-            const double ri = ball ? kBallR : kPlayerR;
-            constexpr double nmB = 1.0 / (kBallMinv + 0.0), nmP = 1.0 / (kPlayerMinv + 0.0);  // b static
-            const SegLds g = sh_->seg[sg];
-            double nx, ny, p1x, p1y, p2x, p2y;
-            cs_contact(pi_.x, pi_.y, ri, g, nx, ny, p1x, p1y, p2x, p2y);
-            record(i, 32 + sg, i * kNSeg + sg, nx, ny, p1x, p1y, p2x, p2y, pi_.x, pi_.y, vi.x, vi.y, 0.0, 0.0,
-                   0.0, 0.0, ball ? nmB : nmP, kE * 0.0);
-        }
+        hsw[w] = hitm;
     });
 
-    FUTBOL_STAMP(dtc == 2 ? 18 : 9);
-    // (2) circle-circle contacts, pairs (i, j > i) in row-major order
+    // (2) circle-circle hits, pairs (i, j > i) in row-major order q (arbiter id Nb * 12 + q):
+    // cpBBIntersects && dist^2 < (ri + rj)^2 (CircleToCircle's own expressions), branch-free
+    constexpr int PCC = S::Nb * (S::Nb - 1) / 2;
+    constexpr int NPW = (PCC + 63) / 64;
+    uint64_t hpw[NPW];
+    sfor<NPW>([&](auto Q) { hpw[Q] = 0; });
     sfor<S::Nb>([&](auto I) {
         constexpr int i = I;
         constexpr double ri = i == S::BALL ? kBallR : kPlayerR;
-        constexpr double mi = i == S::BALL ? kBallMinv : kPlayerMinv;
         const double cl = e.px[i] - ri, cb = e.py[i] - ri, cr = e.px[i] + ri, ct = e.py[i] + ri;
-        if constexpr (!kCompactPairs) {
-            // few bodies: one branch per pair (i, j > i), compile-time j
-            sfor<i + 1, S::Nb>([&](auto J) {
-                constexpr int j = J;
-                constexpr double rj = j == S::BALL ? kBallR : kPlayerR;
-                constexpr double mj = j == S::BALL ? kBallMinv : kPlayerMinv;
-                if (!(cl <= e.px[j] + rj && e.px[j] - rj <= cr && cb <= e.py[j] + rj && e.py[j] - rj <= ct)) return;
-                double nx, ny, p1x, p1y, p2x, p2y;
-                if (cc_test(e.px[i], e.py[i], ri, e.px[j], e.py[j], rj, nx, ny, p1x, p1y, p2x, p2y)) {
-                    constexpr int pair = S::Nb * kNSeg + i * S::Nb - i * (i + 1) / 2 + (j - i - 1);
-                    constexpr double nm = 1.0 / (mi + mj);
-                    record(i, j, pair, nx, ny, p1x, p1y, p2x, p2y, e.px[i], e.py[i], e.vx[i], e.vy[i], e.px[j],
-                           e.py[j], e.vx[j], e.vy[j], nm, kE * kE);
-                }
-            });
-            return;
-        }
-        // many bodies: the hit test of every pair (i, j > i) (cpBBIntersects && dist^2 < (ri + rj)^2,
-        // CircleToCircle's own expressions) branch-free into a bit mask, then one contact per
-        // set bit in ascending j -- a wave runs max-over-lanes(hits of i) contact bodies instead
-        // of one per j that any lane hits; j's state is gathered from the LDS rows staged above
-        uint32_t hits = 0;
         sfor<i + 1, S::Nb>([&](auto J) {
             constexpr int j = J;
             constexpr double rj = j == S::BALL ? kBallR : kPlayerR;
+            constexpr int q = i * S::Nb - i * (i + 1) / 2 + (j - i - 1);
             const bool bb = cl <= e.px[j] + rj && e.px[j] - rj <= cr && cb <= e.py[j] + rj && e.py[j] - rj <= ct;
             const double mind = ri + rj;
             const double dx = e.px[j] - e.px[i], dy = e.py[j] - e.py[i];
-            hits |= (bb && dx * dx + dy * dy < mind * mind) ? 1u << j : 0u;
+            hpw[q / 64] |= (bb && dx * dx + dy * dy < mind * mind) ? 1ull << (q % 64) : 0ull;
         });
-        constexpr int pair0 = S::Nb * kNSeg + i * S::Nb - i * (i + 1) / 2 - i - 1;  // pair id of (i, j) = pair0 + j
-        while (hits) {
-            const int j = __builtin_ctz(hits);
-            hits &= hits - 1;
-            const double2 pj = sh_->vb(j, ln_), vj = sh_->v(j, ln_);
-            const bool ball_j = j == S::BALL;
-            const double rj = ball_j ? kBallR : kPlayerR;
-            constexpr double nmB = 1.0 / (mi + kBallMinv), nmP = 1.0 / (mi + kPlayerMinv);
-            double nx, ny, p1x, p1y, p2x, p2y;
-            cc_contact(e.px[i], e.py[i], ri, pj.x, pj.y, rj, nx, ny, p1x, p1y, p2x, p2y);
-            record(i, j, pair0 + j, nx, ny, p1x, p1y, p2x, p2y, e.px[i], e.py[i], e.vx[i], e.vy[i], pj.x, pj.y,
-                   vj.x, vj.y, ball_j ? nmB : nmP, kE * kE);
-        }
     });
+    FUTBOL_STAMP(dtc == 2 ? 18 : 9);
+
+    // (3) contacts and records.  A hit's record slot is its rank in canonical order (segment hits,
+    // then pair hits).  The hits of all active lanes are one work list: lane l's hits occupy
+    // entries [base_l, base_l + hits_l) of a table in the static row Z (unused until the solve),
+    // and active lane w computes entries w, w + A, ... -- the contact of one (env, hit) each,
+    // written into slot r of env column o -- so a wave computes ceil(total hits / A) contacts per
+    // lane instead of max-over-lanes(hits).  The owners then attach the cached jnAcc / NORMAL
+    // state (their preloaded cache entries are registers).  Beyond the table's capacity the
+    // lanes compute their own contacts (same arithmetic, same records).
+    int nh = 0;
+    sfor<NWS>([&](auto WD) { nh += __popcll(hsw[WD]); });
+    sfor<NPW>([&](auto Q) { nh += __popcll(hpw[Q]); });
+    constexpr int kTableCap = EPW * (int)sizeof(double2) / 4;  // u32 entries in row Z
+    uint32_t base = 0, total = 0;
+#pragma unroll
+    for (int b = 0; b < 9; ++b) {  // wave exclusive prefix of nh (nh <= P < 512)
+        const uint64_t mb = __ballot((nh >> b) & 1);
+        base += __builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, 0u)) << b;
+        total += (uint32_t)__popcll(mb) << b;
+    }
+    auto pid_of = [&](int word, int bit, bool segw) {  // arbiter id of a hit bit
+        return segw ? word * BPW * kNSeg + bit : S::Nb * kNSeg + word * 64 + bit;
+    };
+    // the contact and record of hit `pid` of env column o (env id oenv), record slot r
+    auto contact = [&](int o, int oenv, int pid, int r, bool attach) {
+        double nx, ny, p1x, p1y, p2x, p2y, apx, apy, avx, avy, bpx = 0.0, bpy = 0.0, bvx_ = 0.0, bvy_ = 0.0, nMass, ee;
+        int a, bcode;
+        if (pid < S::Nb * kNSeg) {  // circle (body a) - segment sg: b is the static body
+            a = pid / kNSeg;
+            const int sg = pid - a * kNSeg;
+            const double2 pa = sh_->vb(a, o), va = sh_->v(a, o);
+            const bool ball = a == S::BALL;
+            constexpr double nmB = 1.0 / (kBallMinv + 0.0), nmP = 1.0 / (kPlayerMinv + 0.0);
+            cs_contact(pa.x, pa.y, ball ? kBallR : kPlayerR, sh_->seg[sg], nx, ny, p1x, p1y, p2x, p2y);
+            apx = pa.x; apy = pa.y; avx = va.x; avy = va.y;
+            nMass = ball ? nmB : nmP;
+            ee = kE * 0.0;
+            bcode = 32 + sg;
+        } else {  // circle pair (a, b), a < b: a is a player (the ball is the last body)
+            const int q = pid - S::Nb * kNSeg;
+            int i = 0;
+            sfor<1, S::Nb - 1>([&](auto K) {
+                constexpr int k = K;
+                i += q >= k * S::Nb - k * (k + 1) / 2 ? 1 : 0;
+            });
+            const int j = q - (i * S::Nb - i * (i + 1) / 2) + i + 1;
+            const double2 pa = sh_->vb(i, o), va = sh_->v(i, o), pb = sh_->vb(j, o), vb = sh_->v(j, o);
+            const bool ball_j = j == S::BALL;
+            constexpr double nmB = 1.0 / (kPlayerMinv + kBallMinv), nmP = 1.0 / (kPlayerMinv + kPlayerMinv);
+            cc_contact(pa.x, pa.y, kPlayerR, pb.x, pb.y, ball_j ? kBallR : kPlayerR, nx, ny, p1x, p1y, p2x, p2y);
+            apx = pa.x; apy = pa.y; avx = va.x; avy = va.y;
+            bpx = pb.x; bpy = pb.y; bvx_ = vb.x; bvy_ = vb.y;
+            nMass = ball_j ? nmB : nmP;
+            ee = kE * kE;
+            a = i;
+            bcode = j;
+        }
+        // cpArbiterUpdate + preStep (needs the pre-damping v)
+        const double r1x = p1x - apx, r1y = p1y - apy;
+        const double r2x = p2x - bpx, r2y = p2y - bpy;
+        const double bdx = bpx - apx, bdy = bpy - apy;
+        const double dist = ((r2x - r1x) + bdx) * nx + ((r2y - r1y) + bdy) * ny;
+        double m = dist + slop;
+        m = (0.0 < m) ? 0.0 : m;
+        const double bias = cdiv(-biasCoef * m, dt, rdt);
+        const double bounce = ((bvx_ - avx) * nx + (bvy_ - avy) * ny) * ee;
+        double jn = 0.0;
+        bool normal = false;
+        if (attach) {  // own record: the preloaded cache entries
+#pragma unroll
+            for (int c = 0; c < CKN<N>; ++c)
+                if ((int)(ck[c] & 0x3ffu) == pid) {
+                    jn = cj[c];
+                    normal = (ck[c] >> 12) == 0;  // touched by the previous step: NORMAL -> warm start
+                    touched |= 1u << c;
+                }
+        }
+        FB_BOUND(L, r < S::P && pid < S::P, 5, r = S::P - 1);
+        const double2 q0 = make_double2(nx, ny), q1 = make_double2(nMass, __longlong_as_double(pack_info(a, bcode, pid, normal))),
+                      q2 = make_double2(bias, -bounce), q3 = make_double2(0.0, jn);
+        if (r < KLs) {
+            sh_->rec[r][0][o] = q0;
+            sh_->rec[r][1][o] = q1;
+            sh_->rec[r][2][o] = q2;
+            sh_->rec[r][3][o] = q3;
+        } else {
+            double* sp0 = L.spill + (size_t)(r - KLs) * 8 * B + oenv;
+            sp0[0 * (size_t)B] = q0.x;
+            sp0[1 * (size_t)B] = q0.y;
+            sp0[2 * (size_t)B] = q1.x;
+            sp0[3 * (size_t)B] = q1.y;
+            sp0[4 * (size_t)B] = q2.x;
+            sp0[5 * (size_t)B] = q2.y;
+            sp0[6 * (size_t)B] = q3.x;
+            sp0[7 * (size_t)B] = q3.y;
+        }
+    };
+    n = nh;
+    if (total <= (uint32_t)kTableCap) {
+        uint32_t* const table = reinterpret_cast<uint32_t*>(&sh_->rows[S::Nb][0]);
+        {   // publish this lane's hits: (lane | arbiter id << 6 | slot << 16)
+            uint32_t r = 0;
+            sfor<NWS>([&](auto WD) {
+                uint64_t h = hsw[WD];
+                while (h) {
+                    const int bit = __builtin_ctzll(h);
+                    h &= h - 1;
+                    table[base + r] = (uint32_t)ln_ | ((uint32_t)pid_of(WD, bit, true) << 6) | (r << 16);
+                    ++r;
+                }
+            });
+            sfor<NPW>([&](auto Q) {
+                uint64_t h = hpw[Q];
+                while (h) {
+                    const int bit = __builtin_ctzll(h);
+                    h &= h - 1;
+                    table[base + r] = (uint32_t)ln_ | ((uint32_t)pid_of(Q, bit, false) << 6) | (r << 16);
+                    ++r;
+                }
+            });
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint64_t live = __ballot(1);
+        const uint32_t A = (uint32_t)__popcll(live);
+        const uint32_t w0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
+        for (uint32_t it = w0; it < total; it += A) {
+            const uint32_t en = table[it];
+            const int o = (int)(en & 63u);
+            contact(o, env - ln_ + o, (int)((en >> 6) & 1023u), (int)(en >> 16), false);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // the owner attaches the cached jnAcc and the NORMAL (warm start) flag to its records
+        for (int s = 0; s < n; ++s) {
+            const double2 r1 = L.get(s, 1);
+            const int pid = (int)((__double_as_longlong(r1.y) >> 11) & 511);
+            double jn = 0.0;
+            bool hit = false, normal = false;
+#pragma unroll
+            for (int c = 0; c < CKN<N>; ++c)
+                if ((int)(ck[c] & 0x3ffu) == pid) {
+                    jn = cj[c];
+                    hit = true;
+                    normal = (ck[c] >> 12) == 0;
+                    touched |= 1u << c;
+                }
+            if (hit) {
+                L.put(s, 3, make_double2(0.0, jn));
+                if (normal)
+                    L.put(s, 1, make_double2(r1.x, __longlong_as_double(__double_as_longlong(r1.y) | (1ll << 20))));
+            }
+        }
+    } else {  // more hits than table entries: every lane computes its own contacts
+        int r = 0;
+        sfor<NWS>([&](auto WD) {
+            uint64_t h = hsw[WD];
+            while (h) {
+                const int bit = __builtin_ctzll(h);
+                h &= h - 1;
+                contact(ln_, env, pid_of(WD, bit, true), r, true);
+                ++r;
+            }
+        });
+        sfor<NPW>([&](auto Q) {
+            uint64_t h = hpw[Q];
+            while (h) {
+                const int bit = __builtin_ctzll(h);
+                h &= h - 1;
+                contact(ln_, env, pid_of(Q, bit, false), r, true);
+                ++r;
+            }
+        });
+    }
 
     FUTBOL_CRUMB(L, 40 + dtc);
     FUTBOL_STAMP(dtc == 2 ? 4 : 9);
