@@ -118,6 +118,7 @@ def stamps_report(venv, one_step, args):
            "segment_candidate_iterations_per_wave_step": per[24], "segment_contact_iterations_per_wave_step": per[25]}
     # single-launch snapshots: wave start/end (100 MHz realtime), cycles, placement
     snaps = []
+    waves = []  # per-wave slots of every snapshot launch (tail study: --stamps-dump)
     slow = np.zeros(STAMP_STRIDE)
     for k in range(args.snapshots):
         for _ in range(args.snapshot_stride - 1):
@@ -127,6 +128,7 @@ def stamps_report(venv, one_step, args):
         torch.cuda.synchronize()
         nat.check(nat.load().futbol_debug_stamps(venv.ctx.h, buf.ctypes.data, buf.size, 0), venv.ctx.h)
         w = buf[:nblk * STAMP_STRIDE].reshape(nblk, STAMP_STRIDE)
+        waves.append(w.copy())
         slow += w[int(np.argmax(w[:, 13]))].astype(np.float64)   # phases of this launch's slowest wave
         t0_, t1_, cyc, hw = (w[:, 11].astype(np.float64), w[:, 12].astype(np.float64),
                              w[:, 13].astype(np.float64), w[:, 14])
@@ -142,6 +144,8 @@ def stamps_report(venv, one_step, args):
     rep["slowest_wave_records"] = slow[15] / max(len(snaps), 1)
     rep["snapshots"] = snaps
     rep["snapshot_mean"] = {k: float(np.mean([x[k] for x in snaps])) for k in snaps[0]} if snaps else None
+    if args.stamps_dump:
+        np.save(args.stamps_dump, np.stack(waves))
     print(json.dumps(rep, indent=1))
     venv.close()
 
@@ -166,6 +170,8 @@ def main():
                     help="steps timed per-kernel with HIP events (a multiple of the episode length)")
     ap.add_argument("--snapshots", type=int, default=24, help="--stamps: single-launch wave snapshots")
     ap.add_argument("--snapshot-stride", type=int, default=5, help="--stamps: steps between snapshots")
+    ap.add_argument("--stamps-dump", default="",
+                    help="--stamps: save every snapshot's per-wave slots [snapshots, waves, 32] to this .npy")
     ap.add_argument("--stamps", action="store_true",
                     help="diagnostic: load the FUTBOL_STAMPS build and print the per-phase cycle breakdown")
     args = ap.parse_args()

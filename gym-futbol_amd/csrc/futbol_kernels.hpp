@@ -35,6 +35,7 @@ struct V1Params {
     double biasc[3];                              // 1 - cpfpow(collisionBias, dt)
     double slop;                                  // collisionSlop (0.1f)
     double clamp2_player, clamp2_ball;            // largest s with RN(sqrt(s)) <= vmax (limit_velocity)
+    double form_vb;                               // formation micro-step: |v_bias| bound of the no-contact fast path
     uint64_t seed;
     uint32_t env_base;                            // global id of env 0
     int B;

@@ -69,8 +69,16 @@ constexpr int CBN = N >= 5 ? 1 : 4;
         }                                                                                                 \
         _stamp_prev = _t;                                                                                 \
     } while (0)
+// wave-uniform event counts for the tail study (slots 26-31): added once per wave by lane 0
+#define FUTBOL_STAT(slot, val)                                                                            \
+    do {                                                                                                  \
+        const unsigned long long _v = (unsigned long long)(val);                                          \
+        if ((threadIdx.x & 63) == 0 && st_stamps)                                                         \
+            atomicAdd(&st_stamps[(size_t)(blockIdx.x * EPW / 64) * kStampStride + (slot)], _v);           \
+    } while (0)
 #else
 #define FUTBOL_STAMP(slot) do { } while (0)
+#define FUTBOL_STAT(slot, val) do { } while (0)
 #endif
 
 // Diagnostic builds only.
@@ -631,6 +639,12 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
         }
     };
     n = nh;
+    if (dtc == 2) {
+        FUTBOL_STAT(26, total);
+        FUTBOL_STAT(27, total > (uint32_t)kTableCap ? 1 : 0);
+        FUTBOL_STAT(28, __ballot(ncache > (uint32_t)CKN<N>) ? 1 : 0);
+        FUTBOL_STAT(29, __ballot(n > KLs) ? 1 : 0);
+    }
     if (total <= (uint32_t)kTableCap) {
         uint32_t* const table = reinterpret_cast<uint32_t*>(&sh_->rows[S::Nb][0]);
         {   // publish this lane's hits: (lane | arbiter id << 6 | slot << 16)
@@ -983,6 +997,62 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
     FUTBOL_STAMP(dtc == 2 ? 7 : 9);
 }
 
+// cpSpaceStep(1e-4) right after _position_to_initial (v = 0, p = formation), when provably no
+// pair collides (every |v_bias| component below P.form_vb, futbol_v1_params.hpp): the same state
+// space_step computes with zero contacts -- positions integrated with the carried v_bias (D.2),
+// v_bias cleared, v = +0 damped (+0), no solve, and the arbiter cache filtered (every entry
+// untouched: age + 1, dropped at 3, compacted in order).  Returns false, having changed nothing,
+// when the guard fails; the caller then runs space_step.  No LDS, no wave-level operation: it
+// runs on whichever lanes need it (a goal lane's restart costs a few hundred cycles instead of a
+// whole narrowphase).
+template <int N, int EPW>
+__device__ __forceinline__ bool formation_step(const V1Params& P, const Lane<N, EPW>& L, Env<N>& e)
+{
+    using S = V1Shape<N>;
+    bool ok = true;
+    sfor<S::Nb>([&](auto K) {
+        constexpr int k = K;
+        ok = ok && __builtin_fabs(e.bx[k]) < P.form_vb && __builtin_fabs(e.by[k]) < P.form_vb;
+    });
+    if (!ok) return false;
+    const double dt = P.dtv[1], damping = P.damp[1];
+    sfor<S::Nb>([&](auto K) {  // cpBodyUpdatePosition, cpBodyUpdateVelocity (s2 = 0: no clamp)
+        constexpr int k = K;
+        e.px[k] = e.px[k] + (e.vx[k] + e.bx[k]) * dt;
+        e.py[k] = e.py[k] + (e.vy[k] + e.by[k]) * dt;
+        e.bx[k] = 0.0;
+        e.by[k] = 0.0;
+        e.vx[k] = e.vx[k] * damping + 0.0 * dt;
+        e.vy[k] = e.vy[k] * damping + 0.0 * dt;
+    });
+    e.meta.set_dtcode(1);
+    // cpSpaceArbiterSetFilter with no contact: survivors keep their order, age + 1 < 3
+    const uint32_t ncache = e.meta.ncache();
+    const int B = L.B, env = L.env;
+    uint32_t w = 0;
+    for (uint32_t c0 = 0; c0 < ncache; c0 += 4) {
+        uint32_t key[4];
+        double jn[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {  // 4 independent loads, clamped in bounds
+            const uint32_t c = c0 + i < (uint32_t)S::P ? c0 + i : (uint32_t)S::P - 1;
+            key[i] = L.ckey[(size_t)c * B + env];
+            jn[i] = L.cjn[(size_t)c * B + env];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t age = key[i] >> 12;
+            if (c0 + i < ncache && age + 1 < 3) {
+                L.ckey[(size_t)w * B + env] = (uint16_t)((key[i] & 0x3ffu) | ((age + 1) << 12));
+                L.cjn[(size_t)w * B + env] = jn[i];
+                ++w;
+            }
+        }
+    }
+    e.meta.set_ncache(w);
+    return true;
+}
+
 // ---------------------------------------------------------------------------
 template <int N>
 __device__ __forceinline__ void position_to_initial(const V1Params& P, Env<N>& e)
@@ -1082,6 +1152,7 @@ __device__ __forceinline__ void do_reset(const V1Params& P, const V1Params* __re
     e.meta.set_owner((uint32_t)rs.choice(2));
     e.meta.set_steps(0);
     position_to_initial<N>(P, e);
+    if (formation_step<N, EPW>(P, L, e)) return;
     uint32_t ck[CKN<N>];
     double cj[CKN<N>];
     load_cache_pre<N, EPW>(L, e.meta.ncache(), ck, cj);
@@ -1103,7 +1174,16 @@ __device__ __forceinline__ void pass_target(const Env<N>& e, Stream& rs, int ar,
         ty = e.py[base];
         return;
     } else {
-        int t = rs.choice(N - 1);  // random.choices over teammates != self
+        // random.choices over teammates != self.  With one teammate (N = 2) every choice of this
+        // function is over one item: floor(u * 1) = 0 for every u in [0, 1), so the draw only
+        // advances the stream (no Philox block is computed) -- the same values and draw order
+        int t;
+        if constexpr (N - 1 == 1) {
+            rs.skip(1);
+            t = 0;
+        } else {
+            t = rs.choice(N - 1);
+        }
         t = t >= me ? t + 1 : t;
         if (ar != 0) {
             const double x0 = e.px[base + me], y0 = e.py[base + me];
@@ -1116,7 +1196,13 @@ __device__ __forceinline__ void pass_target(const Env<N>& e, Stream& rs, int ar,
                 cnt += dir_ok(e.px[base + q] - x0, e.py[base + q] - y0) ? 1 : 0;
             });
             if (cnt > 0) {
-                int pick = rs.choice(cnt);
+                int pick;
+                if constexpr (N - 1 == 1) {  // cnt = 1 (self never qualifies: strict inequalities)
+                    rs.skip(1);
+                    pick = 0;
+                } else {
+                    pick = rs.choice(cnt);
+                }
                 sfor<N>([&](auto Q) {
                     constexpr int q = Q;
                     if (dir_ok(e.px[base + q] - x0, e.py[base + q] - y0)) {
@@ -1317,6 +1403,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
         }
     }
     e.meta.set_owner(owner);
+    FUTBOL_STAT(30, __popcll(__ballot(out)));
     FUTBOL_CRUMB(L, 3);
     FUTBOL_STAMP(2);
 
@@ -1344,12 +1431,15 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
             position_to_initial<N>(P, e);
         }
         FUTBOL_STAMP(ph == 0 ? 3 : 9);
-        if (ph != 0) load_cache_pre<N, EPW>(L, e.meta.ncache(), ck, cj);  // the cache the previous phase left behind
-        space_step<N, EPW>(P, L, e, ph == 0 ? 2 : 1, ck, cj
+        // the restart micro-steps: the per-lane no-contact path unless a v_bias is huge
+        if (ph == 0 || !formation_step<N, EPW>(P, L, e)) {
+            if (ph != 0) load_cache_pre<N, EPW>(L, e.meta.ncache(), ck, cj);  // the cache the previous phase left behind
+            space_step<N, EPW>(P, L, e, ph == 0 ? 2 : 1, ck, cj
 #ifdef FUTBOL_STAMPS
-                      , st_stamps, _stamp_prev
+                          , st_stamps, _stamp_prev
 #endif
-        );
+            );
+        }
         if (ph == 0) {
             if (!out) {  // get_team_reward + get_ball_reward (:493-515)
                 double mx = 0.0;
@@ -1375,6 +1465,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
                 for (int s = 6; s < 12; ++s) goal = goal || cs_hit(P, s, e.px[BL], e.py[BL], kBallR);
             }
             if (goal) r = r + (e.px[BL] > W - 2 ? 1000.0 : -1000.0);
+            FUTBOL_STAT(31, __popcll(__ballot(goal)));
             // current_time += 0.1; done = current_time > total_time
             uint32_t steps = e.meta.steps() + 1;
             steps = steps > (uint32_t)kMaxSteps ? (uint32_t)kMaxSteps : steps;  // saturate (no auto-reset)

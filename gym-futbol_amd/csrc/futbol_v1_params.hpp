@@ -105,6 +105,32 @@ constexpr V1Params v1_params_geometry(int N, double W, double H, const V1Pow& pw
     p.slop = (double)0.1f;
     p.clamp2_player = pw.clamp2_player;
     p.clamp2_ball = pw.clamp2_ball;
+    // The reset micro-step (space.step(1e-4) right after _position_to_initial) moves body k from
+    // its formation point by v_bias_k * 1e-4 and nothing else (v = 0).  clear = a lower bound of
+    // every surface gap at formation -- body pairs and body-segment pairs, from per-axis distances
+    // (Euclidean >= each axis's) -- so a step in which every |v_bias| component stays below
+    // clear / 4 / 1e-4 moves each body by less than clear / 2 (sqrt(2) / 4 < 1 / 2) and provably
+    // collides nothing.  0 (fast path off) when the formation itself is crowded.
+    const int Nb = 2 * N + 1;
+    double clear = 1e300;
+    for (int i = 0; i < Nb; ++i) {
+        const double ri = i == 2 * N ? 1.0 : 1.5;  // Ball / Player radius
+        for (int j = i + 1; j < Nb; ++j) {
+            const double rj = j == 2 * N ? 1.0 : 1.5;
+            const double ax = p.fx[i] < p.fx[j] ? p.fx[j] - p.fx[i] : p.fx[i] - p.fx[j];
+            const double ay = p.fy[i] < p.fy[j] ? p.fy[j] - p.fy[i] : p.fy[i] - p.fy[j];
+            const double g = (ax > ay ? ax : ay) - (ri + rj);
+            clear = g < clear ? g : clear;
+        }
+        for (int s = 0; s < 12; ++s) {
+            const double l = p.sl[s] + 1.0, r = p.sr[s] - 1.0, b = p.sb[s] + 1.0, t = p.st[s] - 1.0;
+            const double ax = p.fx[i] < l ? l - p.fx[i] : (p.fx[i] > r ? p.fx[i] - r : 0.0);
+            const double ay = p.fy[i] < b ? b - p.fy[i] : (p.fy[i] > t ? p.fy[i] - t : 0.0);
+            const double g = (ax > ay ? ax : ay) - (ri + 1.0);  // segment radius 1
+            clear = g < clear ? g : clear;
+        }
+    }
+    p.form_vb = clear > 1.0 ? clear * 0.25 * 1e4 : 0.0;
     return p;
 }
 

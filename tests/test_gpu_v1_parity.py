@@ -203,3 +203,68 @@ def test_custom_field_size():
     venv = FutbolVecEnv("v1", B, seed=3, dtype=torch.float64, number_of_player=n, width=90, height=60)
     _rollout_equal(venv, O.V1Vec(B, N=n, seed=3, width=90.0, height=60.0, portable=True), n, B, 320, "90x60")
     venv.close()
+
+
+@pytest.mark.parametrize("n,B", [(2, 512), (5, 256)])
+def test_goal_restart_micro_step(n, B):
+    """A goal's restart micro-step (space.step(1e-4) from formation) runs the per-lane no-contact
+    path: teacher-forced states with the ball about to cross the right goal line (or the left
+    one), random v_bias and random cached arbiters of every age, compared with the oracle
+    right after the goal step (arbiter ages and compaction included) and for a few steps more."""
+    seed = 300 + n
+    ora = _crowded_states(n, B, seed)
+    rng = np.random.default_rng(seed + 1)
+    nb = 2 * n + 1
+    for i in range(B):
+        e = ora.envs[i]
+        right = i % 2 == 0
+        e.px[nb - 1], e.py[nb - 1] = (103.8 if right else 1.2), 34 + rng.uniform(-6, 6)
+        e.vx[nb - 1], e.vy[nb - 1] = (18.0 if right else -18.0), 0.0
+        for k in range(nb - 1):  # players out of the way of the ball
+            e.px[k], e.py[k] = rng.uniform(20, 85), rng.uniform(5, 63)
+    venv = _venv(n, B, seed)
+    venv.set_state(v1_oracle_to_state(ora.envs, n, B))
+    v1_state_to_oracle(venv.get_state(), ora.envs, n, B)
+    a = torch.zeros((B, 2 * n), dtype=torch.uint8, device=venv.device)  # left team: noop
+    for t in range(4):
+        obs, rew, done, _ = venv.step(a)
+        o2, r2, d2, _ = ora.step(a.cpu().numpy().astype(np.int32))
+        r1 = rew.cpu().numpy()
+        if t == 0:
+            assert (np.abs(r1) > 500).mean() > 0.9, "most envs must score on the first step"
+        assert np.array_equal(r1.view(np.uint64), r2.view(np.uint64))
+        assert np.array_equal(obs.cpu().numpy().view(np.uint64), o2.view(np.uint64))
+        _compare_state(venv, ora, n, B, "goal step %d" % t)
+    venv.close()
+
+
+@pytest.mark.parametrize("n,B", [(2, 512), (5, 128)])
+def test_reset_with_large_v_bias(n, B):
+    """reset() keeps v_bias; with |v_bias| beyond the no-contact bound of the
+    formation micro-step (half of the envs, ~1e5) the bodies move by ~10 in space.step(1e-4)
+    and may collide, so those lanes take the full cpSpaceStep: both paths vs the oracle."""
+    seed = 500 + n
+    ora = _crowded_states(n, B, seed)
+    rng = np.random.default_rng(seed)
+    nb = 2 * n + 1
+    for i in range(B):
+        e = ora.envs[i]
+        s = 1e5 if i % 2 else 5.0
+        for k in range(nb):
+            e.bx[k], e.by[k] = rng.normal(0, s, 2)
+    venv = _venv(n, B, seed)
+    venv.set_state(v1_oracle_to_state(ora.envs, n, B))
+    v1_state_to_oracle(venv.get_state(), ora.envs, n, B)
+    o1 = venv.reset().cpu().numpy()
+    o2 = ora.reset()
+    assert np.array_equal(o1.view(np.uint64), o2.view(np.uint64))
+    _compare_state(venv, ora, n, B, "reset")
+    assert np.abs(o1[1::2, :2]).max() > 0.05, "the large-v_bias envs must have moved off formation"
+    for t in range(3):
+        a = venv.random_actions(t, seed=99)
+        obs, rew, done, _ = venv.step(a)
+        o2, r2, d2, _ = ora.step(a.cpu().numpy().astype(np.int32))
+        assert np.array_equal(obs.cpu().numpy().view(np.uint64), o2.view(np.uint64))
+        assert np.array_equal(rew.cpu().numpy().view(np.uint64), r2.view(np.uint64))
+        _compare_state(venv, ora, n, B, "after reset step %d" % t)
+    venv.close()
