@@ -43,14 +43,17 @@ constexpr double kPlayerR = 1.5, kBallR = 1.0, kSegR = 1.0;
 constexpr double kPlayerMinv = 1.0 / 20.0, kBallMinv = 1.0 / 10.0;
 constexpr double kPlayerVmax = 10.0, kBallVmax = 25.0;
 constexpr double kE = 0.2;  // elasticity of players and ball; segments 0
-// arbiter-cache entries preloaded into registers: 4 for N < 5, FUTBOL_CK_LARGE (8) for every
+// arbiter-cache entries preloaded into registers: FUTBOL_CK_SMALL (6) for N < 5, FUTBOL_CK_LARGE (8) for every
 // N >= 5 (5v5 and 10v10 envs hold more cached arbiters: a lane with more than CKN entries sends
 // its whole wave through the global lookup loops)
 #ifndef FUTBOL_CK_LARGE
 #define FUTBOL_CK_LARGE 8
 #endif
+#ifndef FUTBOL_CK_SMALL
+#define FUTBOL_CK_SMALL 6
+#endif
 template <int N>
-constexpr int CKN = N >= 5 ? FUTBOL_CK_LARGE : 4;
+constexpr int CKN = N >= 5 ? FUTBOL_CK_LARGE : FUTBOL_CK_SMALL;
 // entries beyond CKN read per batch of independent loads (5v5 and up: registers are exhausted)
 template <int N>
 constexpr int CBN = N >= 5 ? 1 : 4;
@@ -109,6 +112,11 @@ constexpr int CBN = N >= 5 ? 1 : 4;
 #define FUTBOL_CRUMB(L, k) do { } while (0)
 #endif
 
+// the split solve works per connected component of an env's contact graph (Nb <= 8: body labels
+// in 4-bit fields, slot masks in 8-bit fields; 5v5 and 10v10 solve each env as one item)
+template <int N>
+constexpr bool kSolveComponents = 2 * N + 1 <= 8;
+
 template <int N>
 struct V1Shape {
     static constexpr int Nb = 2 * N + 1;
@@ -155,9 +163,9 @@ struct Scratch {
     // velocities (v rows) for the per-lane dynamic body index.
     double2 rows[2 * S::Nb + 1][EPW];
     double minv[S::Nb + 1];  // inverse mass by row: players, ball, Z = 0
-    uint8_t item_env[EPW + 1];  // split solve: compacted list of the lanes (envs) with contacts (+ a spare slot)
-    uint16_t item_n[EPW + 1];   // ... and their record counts
-    uint8_t item_pc[EPW + 1];   // ... and the dt code of their previous cpSpaceStep (warm-start dt ratio)
+    // split solve work list (+ a spare entry): env column (6 bits) | LDS record slots (8) << 6 | dt code of
+    // the env's previous cpSpaceStep (warm-start dt ratio, 2) << 14 | the env's record count << 16
+    uint32_t item[EPW + 1];
     SegLds seg[kNSeg];
 
     __device__ __forceinline__ double2& vb(int k, int l) { return rows[k][l]; }
@@ -542,6 +550,55 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
     });
     FUTBOL_STAMP(dtc == 2 ? 18 : 9);
 
+    // (2b) connected components of the env's contact graph for the split solve (Nb <= 8): two
+    // records are connected when they share a dynamic body (segments are the static body, whose
+    // velocity rows stay +0 whatever is applied to them), and the sequential-impulse solve of one
+    // component never reads a row another component writes -- so each component is solved as its
+    // own chain, in canonical record order, with results bit-identical to solving the env's whole
+    // list in order.  cslots: byte c = the LDS record slots (< 8) of the component labelled c
+    // (labels: the lowest body of each component, 4-bit fields of `lab`, merged per pair hit).
+    uint64_t cslots = 0;
+    if constexpr (kSolveComponents<N>) {
+        uint32_t lab = 0;
+        uint64_t osp = 0;  // byte k: the record slots whose first body is k
+        int r = 0;
+        sfor<S::Nb>([&](auto K) {  // body k's segment records: slots [r, r + count)
+            constexpr int k = K;
+            const uint32_t bits = (uint32_t)(hsw[k / BPW] >> (kNSeg * (k % BPW))) & 0xfffu;
+            const int cnt = __popc(bits);
+            const uint32_t rng = r < 8 ? (((1u << (cnt < 8 ? cnt : 8)) - 1u) << r) & 0xffu : 0u;
+            osp |= (uint64_t)rng << (8 * k);
+            lab |= (uint32_t)k << (4 * k);
+            r += cnt;
+        });
+        sfor<NPW>([&](auto Q) {
+            uint64_t h = hpw[Q];
+            while (h) {
+                const int q = Q * 64 + __builtin_ctzll(h);
+                h &= h - 1;
+                int i = 0;
+                sfor<1, S::Nb - 1>([&](auto K) {
+                    constexpr int k = K;
+                    i += q >= k * S::Nb - k * (k + 1) / 2 ? 1 : 0;
+                });
+                const int j = q - (i * S::Nb - i * (i + 1) / 2) + i + 1;
+                osp |= (uint64_t)(r < 8 ? 1u << r : 0u) << (8 * i);
+                ++r;
+                // union: every field labelled max(ci, cj) becomes min(ci, cj) (SWAR zero-field test)
+                const uint32_t ci = (lab >> (4 * i)) & 15u, cj = (lab >> (4 * j)) & 15u;
+                const uint32_t lo = ci < cj ? ci : cj, hi = ci < cj ? cj : ci;
+                const uint32_t x = lab ^ (hi * 0x11111111u);
+                const uint32_t z = ~(((x & 0x77777777u) + 0x77777777u) | x) & 0x88888888u;
+                const uint32_t fm = (z >> 3) * 15u;
+                lab = (lab & ~fm) | ((lo * 0x11111111u) & fm);
+            }
+        });
+        sfor<S::Nb>([&](auto K) {
+            constexpr int k = K;
+            cslots |= ((osp >> (8 * k)) & 0xffu) << (8 * ((lab >> (4 * k)) & 15u));
+        });
+    }
+
     // (3) contacts and records.  A hit's record slot is its rank in canonical order (segment hits,
     // then pair hits).  The hits of all active lanes are one work list: lane l's hits occupy
     // entries [base_l, base_l + hits_l) of a table in the static row Z (unused until the solve),
@@ -776,23 +833,59 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
     {
         // Sequential-impulse solve (cpSpaceStep: warm start, then 10 iterations over the arbiters
         // in canonical order), split in two independent halves per env -- the v_bias / jBias chain
-        // and the v / jnAcc chain (apply_half) -- and spread over the wave's active lanes: the
-        // envs with contacts are compacted into a work list of 2 C items (env, half), and lane w
-        // solves item w (then w + A, ... when 2 C exceeds the A active lanes).  Each item is one
-        // lane's serial chain of (10 + warm start) x records half-applications, so an env's
-        // critical path is half the instructions of a whole application, and lanes without
-        // contacts do the other halves.  Records live in LDS (lanes with fewer records than the
-        // wave's LDS maximum are padded with null records) and past the K LDS slots in the global
-        // spill area; rows and records of env e are column e of the block's LDS arrays.
+        // and the v / jnAcc chain (apply_half) -- and per connected component of the env's contact
+        // graph (cslots above), spread over the wave's active lanes: the (env, component) pairs
+        // are compacted into a work list of 2 C items (env, component, half), and lane w solves
+        // item w (then w + A, ... when 2 C exceeds the A active lanes).  Each item is one lane's
+        // serial chain of (10 + warm start) x records half-applications of its component, so the
+        // wave's critical path is its largest component, not its most crowded env, and lanes
+        // without contacts do the other items.  When the components would not fit one round of
+        // the active lanes, every env is one item (its whole record list).  Records live in LDS
+        // and past the K LDS slots in the global spill area (an env with spill records is always
+        // one item); rows and records of env e are column e of the block's LDS arrays; an item
+        // shorter than the wave's longest is padded with null applications on the static row.
         Scratch<N, EPW>* sh = L.sh;
         const int ln = L.lane;
         constexpr int KL = Lane<N, EPW>::KL;
         const int nf = n < KL ? n : KL;  // records in LDS; slots >= KL are in the global spill
+        const uint64_t act = __ballot(n > 0);
+        const uint64_t live = __ballot(1);
+        const int A = __popcll(live);
+        const int w = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
+        const uint64_t whole = n > 0 ? (1ull << nf) - 1ull : 0ull;  // the env's LDS slots as one item
+        uint64_t cm = whole;
+        uint32_t cbase = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+        int total = __popcll(act);
+        if constexpr (kSolveComponents<N>) {
+            const uint64_t cc = n > KL ? whole : cslots;
+            // nonzero bytes of cc (components of this env), then their wave prefix
+            const uint64_t nzb = ((cc | ((cc & 0x7f7f7f7f7f7f7f7full) + 0x7f7f7f7f7f7f7f7full)) >> 7) & 0x0101010101010101ull;
+            const int nc = __popcll(nzb);
+            uint32_t cb = 0, ct = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {  // nc <= 8
+                const uint64_t mb = __ballot((nc >> b) & 1);
+                cb += __builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, 0u)) << b;
+                ct += (uint32_t)__popcll(mb) << b;
+            }
+            if (2 * (int)ct <= A) {  // components fit one round of items
+                cm = cc;
+                cbase = cb;
+                total = (int)ct;
+            }
+        }
+        // the wave's longest item (records): m
+        int msz = 0;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const int c = __popc((uint32_t)(cm >> (8 * b)) & 0xffu);
+            msz = c > msz ? c : msz;
+        }
         int m = 0;
 #pragma unroll
-        for (int b = 4; b >= 0; --b) {
+        for (int b = 3; b >= 0; --b) {
             const int t = m | (1 << b);
-            if (t <= KL && __ballot(nf >= t)) m = t;
+            if (t <= KL && __ballot(msz >= t)) m = t;
         }
         const bool spill = __ballot(n > KL) != 0;
 #ifdef FUTBOL_STAMPS
@@ -800,48 +893,41 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
             atomicAdd(&st_stamps[(size_t)(blockIdx.x * EPW / 64) * kStampStride + 15], (unsigned long long)m);
 #endif
         if (m > 0) {
-            // every lane publishes its rows and pads its records to m (a lane without contacts
-            // writes its own, unused, column: no divergent branch), and the envs with contacts
-            // enter the compacted work list (the others write the spare slot EPW)
-            const uint64_t act = __ballot(n > 0);
+            // every lane publishes its rows (a lane without contacts writes its own, unused,
+            // column: no divergent branch) and its items (the others write the spare entry EPW)
             sfor<S::Nb>([&](auto K) {
                 constexpr int k = K;
                 sh->v(k, ln) = make_double2(e.vx[k], e.vy[k]);
                 sh->vb(k, ln) = make_double2(0.0, 0.0);
             });
             sh->rows[S::Nb][ln] = make_double2(0.0, 0.0);
-            for (int s = nf; s < m; ++s) {
-                sh->rec[s][0][ln] = make_double2(0.0, 0.0);
-                sh->rec[s][1][ln] = make_double2(0.0, __longlong_as_double(null_info<N>()));
-                sh->rec[s][2][ln] = make_double2(0.0, 0.0);
-                sh->rec[s][3][ln] = make_double2(0.0, 0.0);
-            }
             {
-                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
-                const uint32_t slot = n > 0 ? rank : (uint32_t)EPW;
-                sh->item_env[slot] = (uint8_t)ln;
-                sh->item_n[slot] = (uint16_t)n;
-                sh->item_pc[slot] = (uint8_t)pc;
+                const uint32_t tail = (uint32_t)ln | ((uint32_t)pc << 14) | ((uint32_t)(n < 65535 ? n : 65535) << 16);
+                int idx = 0;
+#pragma unroll
+                for (int b = 0; b < (kSolveComponents<N> ? 8 : 1); ++b) {
+                    const uint32_t byte = (uint32_t)(cm >> (8 * b)) & 0xffu;
+                    const uint32_t slot = byte ? cbase + (uint32_t)idx : (uint32_t)EPW;
+                    sh->item[slot] = tail | (byte << 6);
+                    idx += byte ? 1 : 0;
+                }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             FUTBOL_STAMP(dtc == 2 ? 19 : 9);
-            const uint64_t live = __ballot(1);
-            const int A = __popcll(live);
-            const int w = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
-            const int items = 2 * __popcll(act);
+            const int items = 2 * total;
             constexpr uint32_t ROW = EPW * (uint32_t)sizeof(double2);
             const double coef2 = dt / P.dtv[2], coef1 = dt / P.dtv[1];  // dt / prev_dt, prev_dt != 0
             for (int i0 = 0; i0 < items; i0 += A) {
                 const int it_ = i0 + w;
                 if (it_ < items) {
-                    const int ie = sh->item_env[it_ >> 1];
+                    const uint32_t ent = sh->item[it_ >> 1];
+                    const int ie = (int)(ent & 63u);
                     const int h = it_ & 1;
                     // cpArbiterApplyCachedImpulse's dt ratio of THIS env (its previous step may have
                     // been a 1e-4 reset micro-step)
-                    const uint32_t ipc = sh->item_pc[it_ >> 1];
+                    const uint32_t ipc = (ent >> 14) & 3u;
                     const double dt_coef = ipc == 2 ? coef2 : (ipc == 1 ? coef1 : 0.0);
                     char* const base = (char*)&sh->rows[h ? 2 * S::Nb : 0][ie];
                     const int sgn = h ? -1 : 1;
@@ -856,21 +942,30 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
                         FB_BOUND(L, t >= 0 && t < S::P - KL, 0, t = 0);
                         return L.spill + ((size_t)t * 8 + f) * B + ienv;
                     };
-                    const int nie = spill ? (int)sh->item_n[it_ >> 1] : 0;  // env ie's record count
-                    // the env's LDS records in registers for the whole solve (m is wave-uniform: the
+                    const int nie = spill ? (int)(ent >> 16) : 0;  // env ie's record count
+                    // the item's LDS records in registers for the whole solve (m is wave-uniform: the
                     // q < m guards are scalar branches): only the two body rows of each half-
-                    // application go through LDS on the serial chain
+                    // application go through LDS on the serial chain.  Record q of the item is the
+                    // q-th slot of its mask; past its last one, a null application on the static
+                    // row Z (whose rows stay +0: inverse mass 0) whose accumulator is dropped.
                     double qnx[KL], qny[KL], qnm[KL], qc[KL], qacc[KL], qma[KL], qmb[KL];
                     double2 *qra[KL], *qrb[KL];
                     bool qwarm[KL];
+                    int qslot[KL];
+                    uint32_t mk = (ent >> 6) & 0xffu;
                     sfor<KL>([&](auto Q) {
                         constexpr int q = Q;
                         if (q < m) {
-                            const double2 r0 = sh->rec[q][0][ie], r1 = sh->rec[q][1][ie], r2 = sh->rec[q][2][ie],
-                                          r3 = sh->rec[q][3][ie];
+                            const bool has = mk != 0u;
+                            const int sl = (int)(__builtin_ctz(mk | 0x100u) & 7u);  // slot 0 (a real record) when !has
+                            mk &= mk - 1u;
+                            const double2 r0 = sh->rec[sl][0][ie], r1 = sh->rec[sl][1][ie], r2 = sh->rec[sl][2][ie],
+                                          r3 = sh->rec[sl][3][ie];
                             const unsigned long long info = info_of(r1.y);
                             uint32_t ao, bo;
                             info_rows<N, EPW>(info, ao, bo);
+                            ao = has ? ao : (uint32_t)S::Nb * ROW;
+                            bo = has ? bo : (uint32_t)S::Nb * ROW;
                             qnx[q] = r0.x;
                             qny[q] = r0.y;
                             qnm[q] = r1.x;
@@ -880,7 +975,8 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
                             qrb[q] = row(bo);
                             qma[q] = mass(ao);
                             qmb[q] = mass(bo);
-                            qwarm[q] = h && ((info >> 20) & 1);
+                            qwarm[q] = has && h && ((info >> 20) & 1);
+                            qslot[q] = has ? sl : -1;
                         }
                     });
                     // warm start (cpArbiterApplyCachedImpulse), v half only, record order
@@ -917,9 +1013,9 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
                     }
                     sfor<KL>([&](auto Q) {  // jBias / jnAcc back into the record (the arbiter cache reads jnAcc)
                         constexpr int q = Q;
-                        if (q < m) {
-                            if (h) sh->rec[q][3][ie].y = qacc[q];
-                            else sh->rec[q][3][ie].x = qacc[q];
+                        if (q < m && qslot[q] >= 0) {
+                            if (h) sh->rec[qslot[q]][3][ie].y = qacc[q];
+                            else sh->rec[qslot[q]][3][ie].x = qacc[q];
                         }
                     });
                 }
@@ -1086,7 +1182,7 @@ __device__ __forceinline__ void write_obs(const Env<N>& e, OT* o)
 }
 
 template <int N>
-__device__ __forceinline__ void load_env(const V1Ptrs& st, int env, int B, Env<N>& e)
+__device__ __forceinline__ void load_bodies(const V1Ptrs& st, int env, int B, Env<N>& e)
 {
     sfor<V1Shape<N>::Nb>([&](auto K) {
         constexpr int k = K;
@@ -1098,7 +1194,12 @@ __device__ __forceinline__ void load_env(const V1Ptrs& st, int env, int B, Env<N
         e.bx[k] = st.bx[o];
         e.by[k] = st.by[o];
     });
+}
+template <int N>
+__device__ __forceinline__ void load_env(const V1Ptrs& st, int env, int B, Env<N>& e)
+{
     e.meta.w = st.meta[env];
+    load_bodies<N>(st, env, B, e);
 }
 
 template <int N>
@@ -1117,24 +1218,35 @@ __device__ __forceinline__ void store_env(const V1Ptrs& st, int env, int B, cons
     st.meta[env] = e.meta.w;
 }
 
-// the block's segment table in LDS (per-lane dynamic segment index in the collide loop)
+// the block's segment table in LDS (per-lane dynamic segment index in the collide loop), in two
+// halves: fetch_seg issues lane s's loads (lanes 0..11) and store_seg writes them with the solver's
+// inverse-mass table and synchronises -- so that the step kernel can issue these loads ahead of
+// the state's and wait for them alone
+__device__ __forceinline__ SegLds fetch_seg(const V1Params& P)
+{
+    const int s = threadIdx.x < kNSeg ? (int)threadIdx.x : 0;
+    SegLds g;
+    g.ax = P.sax[s];
+    g.ay = P.say[s];
+    g.sdx = P.sbx[s] - P.sax[s];
+    g.sdy = P.sby[s] - P.say[s];
+    g.L2 = P.L2[s];
+    g.rL2 = P.rL2[s];
+    return g;
+}
 template <int N, int EPW>
-__device__ __forceinline__ void load_seg_table(const V1Params& P, Scratch<N, EPW>& sh)
+__device__ __forceinline__ void store_seg(const SegLds& g, Scratch<N, EPW>& sh)
 {
     const int s = threadIdx.x;
-    if (s < kNSeg) {
-        SegLds g;
-        g.ax = P.sax[s];
-        g.ay = P.say[s];
-        g.sdx = P.sbx[s] - P.sax[s];
-        g.sdy = P.sby[s] - P.say[s];
-        g.L2 = P.L2[s];
-        g.rL2 = P.rL2[s];
-        sh.seg[s] = g;
-    }
+    if (s < kNSeg) sh.seg[s] = g;
     if (s <= V1Shape<N>::Nb)  // inverse masses by solver row (Player/Ball mass, static Z)
         sh.minv[s] = s == V1Shape<N>::Nb ? 0.0 : (s == V1Shape<N>::BALL ? kBallMinv : kPlayerMinv);
     __syncthreads();
+}
+template <int N, int EPW>
+__device__ __forceinline__ void load_seg_table(const V1Params& P, Scratch<N, EPW>& sh)
+{
+    store_seg<N, EPW>(fetch_seg(P), sh);
 }
 
 // Futbol.reset (envs_v1/futbol_env.py:146-150): owner draw, formation, space.step(1e-4)
@@ -1256,17 +1368,11 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
     unsigned long long _stamp_prev = __builtin_amdgcn_s_memtime();
     const unsigned long long _wave_real0 = __builtin_amdgcn_s_memrealtime(), _wave_cyc0 = _stamp_prev;
 #endif
-    // every HBM read of the step is issued here, in one batch, before the segment table's
-    // barrier: the body state, the first CK arbiter-cache entries and the running return
-    // (one memory round trip per step)
-    Env<N> e;
-    load_env<N>(st, env, B, e);
-    uint32_t ck[CKN<N>];
-    double cj[CKN<N>];
-    load_cache_pre<N, EPW>(L, e.meta.ncache(), ck, cj);
-    const double ep_ret0 = st.ep_ret[env];
-    // the left team's actions: 2N bytes per env, as 32-bit words when 2N % 4 == 0 (rows stay
-    // 4-byte aligned), 16-bit words otherwise
+    // every HBM read of the step is issued here, in one batch (one memory round trip per step),
+    // in the order of first use: the segment table (waited for alone at its LDS store), the
+    // actions and the meta word (the opponent's draws need only these), then the body state,
+    // the first CK arbiter-cache entries and the running return
+    const SegLds seg_g = fetch_seg(P);
     uint32_t araw[2 * N];
     if constexpr ((2 * N) % 4 == 0) {
         const uint32_t* a32 = (const uint32_t*)(actions + (size_t)env * (2 * N));
@@ -1284,8 +1390,15 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
             araw[2 * w + 1] = x >> 8;
         });
     }
-    load_seg_table<N, EPW>(P, sh);
-    if (!live) return;
+    Env<N> e;
+    e.meta.w = st.meta[env];
+    load_bodies<N>(st, env, B, e);
+    uint32_t ck[CKN<N>];
+    double cj[CKN<N>];
+    load_cache_pre<N, EPW>(L, e.meta.ncache(), ck, cj);
+    const double ep_ret0 = st.ep_ret[env];
+    // lanes past B (last block) run the action phase on their shadow copy of env B-1 in
+    // registers only (no store, no counter) and leave after the segment table is in LDS
     const double W = P.W, H = P.H;
     FUTBOL_CRUMB(L, 1);
     FUTBOL_STAMP(0);
@@ -1309,7 +1422,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
         const int a = rs.choice(5);
         if constexpr (i & 1) key[N + (i >> 1)] = a; else arrow[N + (i >> 1)] = a;
     });
-    if (bad) atomicAdd(st.invalid, (unsigned long long)bad);
+    if (bad && live) atomicAdd(st.invalid, (unsigned long long)bad);
     FUTBOL_STAMP(1);
 
     // _ball_to_team_distance_arr(team_A), ball_init (:433-435)
@@ -1347,7 +1460,19 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
         const bool press = ky == 3 && !tk && ar == 0;   // (:371-391)
         const bool pass = ky == 4 && tk;                // (:394-419)
         double tx = 0.0, ty = 0.0;
-        if (pass) pass_target<N, side, k - side * N>(e, rs, ar, tx, ty);
+        if constexpr (N == 2) {
+            // one teammate: get_pass_target_teammate always returns it (team.py:136-180); its
+            // draws are one-item choices (floor(u * 1) = 0) that only advance the stream: one,
+            // plus one when an arrow is held and the teammate lies strictly that way
+            constexpr int mate = side * N + (1 - (k - side * N));
+            const double mx = e.px[mate] - e.px[k], my = e.py[mate] - e.py[k];
+            const bool way = (ar == 1 && my > 0) || (ar == 2 && mx > 0) || (ar == 3 && my < 0) || (ar == 4 && mx < 0);
+            tx = e.px[mate];
+            ty = e.py[mate];
+            rs.skip(pass ? (way ? 2u : 1u) : 0u);
+        } else {
+            if (pass) pass_target<N, side, k - side * N>(e, rs, ar, tx, ty);
+        }
         const double gx = side == 0 ? W : 0.0, gy = H / 2;
         const double ox = press ? e.px[k] : e.px[BL], oy = press ? e.py[k] : e.py[BL];
         const double qx = press ? e.px[BL] : (shoot ? gx : tx), qy = press ? e.py[BL] : (shoot ? gy : ty);
@@ -1388,9 +1513,9 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
             e.py[BL] = by0 + dby;
             e.vx[BL] = 0.0;
             e.vy[BL] = 0.0;
-            int pick;
-            if (owner == 1) { pick = rs.choice(N); owner = 0; }
-            else { pick = N + rs.choice(N); owner = 1; }
+            // random.choice of the new owner team's players (one draw either way)
+            const int pick = rs.choice(N) + (owner == 1 ? 0 : N);
+            owner = owner == 1 ? 0 : 1;
             sfor<2 * N>([&](auto Q) {
                 constexpr int q = Q;
                 if (q == pick) {
@@ -1404,6 +1529,9 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
     }
     e.meta.set_owner(owner);
     FUTBOL_STAT(30, __popcll(__ballot(out)));
+    // the segment table's loads were issued with the state's; every lane of the block is here
+    store_seg<N, EPW>(seg_g, sh);
+    if (!live) return;
     FUTBOL_CRUMB(L, 3);
     FUTBOL_STAMP(2);
 

@@ -102,9 +102,9 @@ def _crowded_states(n, B, seed):
         e.stamp = 50
         e.curr_dt = [0.1, 0.0001][int(rng.random() < 0.2)]
         e.current_time = 0.0
-        # up to 3x the kernel's register-preloaded cache entries (4 for N < 5, 8 for N >= 5), so that
+        # up to 3x the kernel's register-preloaded cache entries (6 for N < 5, 8 for N >= 5), so that
         # the lookups and the in-place compaction past the preloaded entries run on the first step
-        ckn = 8 if n >= 5 else 4
+        ckn = 8 if n >= 5 else 6
         for p in rng.choice(P, size=int(rng.integers(0, 3 * ckn + 1)), replace=False):
             p = int(p)
             age = int(rng.integers(0, 3))
@@ -128,7 +128,7 @@ def test_teacher_forced_crowded_states(n, B):
     # the oracle must see exactly the state the kernel got (stamps are relative)
     v1_state_to_oracle(venv.get_state(), ora.envs, n, B)
     ex0, _, _ = v1_dense_cache(venv.get_state(), n, B)
-    assert ex0.sum(1).max() > (8 if n >= 5 else 4), "some env must hold more cache entries than are preloaded"
+    assert ex0.sum(1).max() > (8 if n >= 5 else 6), "some env must hold more cache entries than are preloaded"
     for t in range(3):
         a = venv.random_actions(900 + t, seed=4321)
         obs, rew, done, _ = venv.step(a)
