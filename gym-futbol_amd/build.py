@@ -26,6 +26,14 @@ ARCH = os.environ.get("FUTBOL_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fPIC",
           "-Wall", "-Wno-unused-function", "-I" + os.path.join(ROOT, "include")]
+# SimplifyCFG folds an if/else whose arms cost up to this many instructions into selects: the
+# default (4) leaves the fp64 arms of the action / contact code as divergent branches (~40 cycles
+# each on a wave64); 20 measured best for the 2v2 step (-1.5% step time).  Only for the N <= 3
+# instances: the 5v5 float instance built this way (~500 VGPRs, spills) corrupted its step
+# counter on the GPU (tests/test_gpu_api.py episode lengths), so N >= 5 and v0 keep the default.
+PHI = os.environ.get("FUTBOL_PHI_FOLD", "20")
+PHI_FLAGS = ["-mllvm", "-two-entry-phi-node-folding-threshold=" + PHI, "-mllvm", "-phi-node-folding-threshold=" + PHI]
+PHI_SOURCES = ("futbol_v1_n1_e64.hip", "futbol_v1_n2_e64.hip", "futbol_v1_n3_e64.hip")
 # A/B of compiler options: FUTBOL_EXTRA_CFLAGS="..." (with a FUTBOL_BUILD_VARIANT name)
 CFLAGS += os.environ.get("FUTBOL_EXTRA_CFLAGS", "").split()
 if VARIANT == "stamps":
@@ -50,7 +58,7 @@ def _stale(target, sources):
 def _compile(src, force):
     obj = os.path.join(OBJ, os.path.basename(src) + ".o")
     if force or _stale(obj, [src] + _deps()):
-        cmd = [HIPCC] + CFLAGS + ["-c", src, "-o", obj]
+        cmd = [HIPCC] + CFLAGS + (PHI_FLAGS if os.path.basename(src) in PHI_SOURCES else []) + ["-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("hipcc failed for %s:\n%s\n%s" % (src, " ".join(cmd), r.stderr[-8000:]))

@@ -1417,11 +1417,15 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
         a = a > 4 ? 4 : a;
         if constexpr (i & 1) key[i >> 1] = a; else arrow[i >> 1] = a;
     });
-    sfor<2 * N>([&](auto I) {
-        constexpr int i = I;
-        const int a = rs.choice(5);
-        if constexpr (i & 1) key[N + (i >> 1)] = a; else arrow[N + (i >> 1)] = a;
-    });
+    {   // action_space.sample(): 2N uniform integers in [0, 5), four per Philox block, (w * 5) >> 32
+        Philox4 blk;
+        sfor<2 * N>([&](auto I) {
+            constexpr int i = I;
+            if constexpr (i % 4 == 0) blk = rs.next();
+            const int a = (int)(((uint64_t)blk.x[i % 4] * 5ull) >> 32);
+            if constexpr (i & 1) key[N + (i >> 1)] = a; else arrow[N + (i >> 1)] = a;
+        });
+    }
     if (bad && live) atomicAdd(st.invalid, (unsigned long long)bad);
     FUTBOL_STAMP(1);
 

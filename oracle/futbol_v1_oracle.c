@@ -510,7 +510,9 @@ int orc_v1_step(OrcV1 *e, const int32_t *left, double *obs, double *reward)
     const int N = e->N, ball = 2 * N;
     OracleRng g = { e->seed, e->env_id, e->event++, 0, 0 };
     int right[2 * ORC_MAXN];
-    for (int i = 0; i < 2 * N; ++i) right[i] = oracle_choice(&g, 5); /* action_space.sample() */
+    /* action_space.sample() (futbol_env.py:306-307, :429): 2N uniform integers in [0, 5), four per
+       Philox block (RNG contract: DESIGN.md section 3) */
+    oracle_words_choice(&g, 2 * N, 5, right);
 
     double d0[ORC_MAXN];
     team_a_dist(e, d0);

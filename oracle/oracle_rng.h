@@ -83,6 +83,18 @@ static inline int oracle_choice(OracleRng *g, int n)
     return k > n - 1 ? n - 1 : k;
 }
 
+/* n_draws uniform integers in [0, n) from ceil(n_draws / 4) blocks: value i = (w * n) >> 32 for
+   w = word i % 4 of block i / 4 (the v1 opponent's action_space.sample(), and the synthetic
+   left-agent actions under tag 1) */
+static inline void oracle_words_choice(OracleRng *g, int n_draws, int n, int32_t *out)
+{
+    uint32_t x[4];
+    for (int i = 0; i < n_draws; ++i) {
+        if ((i & 3) == 0) oracle_rng_block(g, x);
+        out[i] = (int32_t)(((uint64_t)x[i & 3] * (uint64_t)n) >> 32);
+    }
+}
+
 static inline int oracle_randint(OracleRng *g, int a, int b)
 {
     return a + oracle_choice(g, b - a + 1);

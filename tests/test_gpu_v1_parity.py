@@ -144,8 +144,9 @@ def test_teacher_forced_crowded_states(n, B):
     venv.close()
 
 
-def test_float32_outputs_are_the_cast_of_float64():
-    B, n = 512, 2
+@pytest.mark.parametrize("n,B", [(2, 512), (5, 128), (10, 64)])
+def test_float32_outputs_are_the_cast_of_float64(n, B):
+    """The float-output kernel instances (the default of make()) against the double ones."""
     a64, a32 = _venv(n, B, 3, torch.float64), _venv(n, B, 3, torch.float32)
     o64, o32 = a64.reset(), a32.reset()
     assert torch.equal(o64.float(), o32)
