@@ -86,6 +86,45 @@ __global__ void __launch_bounds__(64) k_solve(const int* __restrict__ pairs, dou
                 constexpr int q = Q;
                 apply_half(ra[q], rb[q], nx[q], ny[q], nm[q], c[q], ma[q], mb[q], acc[q]);
             });
+    } else if constexpr (VAR == 3 || VAR == 4) {
+        // forwarding by loop-invariant 32-bit lane masks and v_bfi_b32 (no SGPR masks)
+        uint32_t mab[M], maa[M], mbb[M], mba[M];
+        SF<0, M>::run([&](auto Q) {
+            constexpr int q = Q;
+            constexpr int nq = q + 1 < M ? q + 1 : 0;
+            mab[q] = ra[nq] == rb[q] ? ~0u : 0u;
+            maa[q] = ra[nq] == ra[q] ? ~0u : 0u;
+            mbb[q] = rb[nq] == rb[q] ? ~0u : 0u;
+            mba[q] = rb[nq] == ra[q] ? ~0u : 0u;
+        });
+        auto bsel = [](uint32_t m, double x, double y) {  // m ? x : y, bitwise
+            const unsigned long long xi = __double_as_longlong(x), yi = __double_as_longlong(y);
+            const uint32_t lo = ((uint32_t)xi & m) | ((uint32_t)yi & ~m);
+            const uint32_t hi = ((uint32_t)(xi >> 32) & m) | ((uint32_t)(yi >> 32) & ~m);
+            return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+        };
+        double2 ca = *ra[0], cb = *rb[0];
+        for (int it = 0; it < 10; ++it)
+            SF<0, M>::run([&](auto Q) {
+                constexpr int q = Q;
+                constexpr int nq = q + 1 < M ? q + 1 : 0;
+                const double2 la = *ra[nq], lb = *rb[nq];
+                if constexpr (VAR == 4) __builtin_amdgcn_sched_barrier(0);  // issue the prefetch first
+                const double vn = (cb.x - ca.x) * nx[q] + (cb.y - ca.y) * ny[q];
+                const double j = (c[q] - vn) * nm[q];
+                const double old = acc[q];
+                const double t = old + j;
+                const double nacc = t > 0.0 ? t : 0.0;
+                acc[q] = nacc;
+                const double d = nacc - old;
+                const double jx = nx[q] * d, jy = ny[q] * d;
+                const double2 na = make_double2(ca.x + (-jx) * ma[q], ca.y + (-jy) * ma[q]);
+                const double2 nb = make_double2(cb.x + jx * mb[q], cb.y + jy * mb[q]);
+                *ra[q] = na;
+                *rb[q] = nb;
+                ca = make_double2(bsel(mab[q], nb.x, bsel(maa[q], na.x, la.x)), bsel(mab[q], nb.y, bsel(maa[q], na.y, la.y)));
+                cb = make_double2(bsel(mbb[q], nb.x, bsel(mba[q], na.x, lb.x)), bsel(mbb[q], nb.y, bsel(mba[q], na.y, lb.y)));
+            });
     } else {
         bool fab[M], faa[M], fbb[M], fba[M];
         SF<0, M>::run([&](auto Q) {
@@ -149,17 +188,18 @@ static void run(const int* d_pairs, double* out, unsigned long long* cyc, const 
            ms * 1e3);
 }
 
+template <int V>
 static void compare(const int* d, double* o1, double* o2, unsigned long long* cyc)
 {
     hipLaunchKernelGGL((k_solve<4, 0>), dim3(1024), dim3(64), 0, 0, d, o1, cyc);
-    hipLaunchKernelGGL((k_solve<4, 2>), dim3(1024), dim3(64), 0, 0, d, o2, cyc);
+    hipLaunchKernelGGL((k_solve<4, V>), dim3(1024), dim3(64), 0, 0, d, o2, cyc);
     CHECK(hipDeviceSynchronize());
     static double h1[1024 * 64], h2[1024 * 64];
     CHECK(hipMemcpy(h1, o1, sizeof(h1), hipMemcpyDeviceToHost));
     CHECK(hipMemcpy(h2, o2, sizeof(h2), hipMemcpyDeviceToHost));
     int bad = 0;
     for (int i = 0; i < 1024 * 64; ++i) bad += h1[i] != h2[i];
-    printf("variant 0 vs 2 (M=4) differing lanes: %d\n", bad);
+    printf("variant 0 vs %d (M=4) differing lanes: %d\n", V, bad);
 }
 
 int main()
@@ -186,12 +226,22 @@ int main()
     CHECK(hipMemcpy(d, h, n * sizeof(int), hipMemcpyHostToDevice));
     double* out2;
     CHECK(hipMalloc(&out2, 1024 * 64 * sizeof(double)));
-    compare(d, out, out2, cyc);
+    compare<2>(d, out, out2, cyc);
+    compare<3>(d, out, out2, cyc);
+    compare<4>(d, out, out2, cyc);
+    run<4, 4>(d, out, cyc, "prefetch first, bfi");
+    run<2, 4>(d, out, cyc, "prefetch first, bfi");
+    run<1, 4>(d, out, cyc, "prefetch first, bfi");
+    run<8, 4>(d, out, cyc, "prefetch first, bfi");
     run<4, 0>(d, out, cyc, "kernel loop");
-    run<4, 1>(d, out, cyc, "v rows swizzled");
     run<4, 2>(d, out, cyc, "prefetch/forward");
+    run<4, 3>(d, out, cyc, "prefetch/forward bfi");
+    run<2, 0>(d, out, cyc, "kernel loop");
+    run<2, 3>(d, out, cyc, "prefetch/forward bfi");
+    run<1, 0>(d, out, cyc, "kernel loop");
+    run<1, 3>(d, out, cyc, "prefetch/forward bfi");
     run<8, 0>(d, out, cyc, "kernel loop");
-    run<8, 1>(d, out, cyc, "v rows swizzled");
     run<8, 2>(d, out, cyc, "prefetch/forward");
+    run<8, 3>(d, out, cyc, "prefetch/forward bfi");
     return 0;
 }
