@@ -30,6 +30,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 #include "futbol_kernels.hpp"
 #include "futbol_v1_params.hpp"
 #include "futbol_rng.hpp"
@@ -112,8 +113,13 @@ constexpr int CBN = N >= 5 ? 1 : 4;
 #define FUTBOL_CRUMB(L, k) do { } while (0)
 #endif
 
-// the split solve works per connected component of an env's contact graph (Nb <= 8: body labels
-// in 4-bit fields, slot masks in 8-bit fields; 5v5 and 10v10 solve each env as one item)
+// the split solve works per connected component of an env's contact graph: body labels in 4-bit
+// fields (Nb <= 16), slot masks in kSlotBits-bit fields of a u64 (8 bits for Nb <= 8, 4 bits for
+// the 5v5 instance's 4 LDS slots).  Enabled for N <= 3: the 5v5 instance measured 2% slower with
+// it (its tail waves are envs past the LDS record slots, solved as one item anyway), 10v10 has
+// more bodies than 4-bit labels hold
+template <int N>
+constexpr int kSlotBits = 2 * N + 1 <= 8 ? 8 : 4;
 template <int N>
 constexpr bool kSolveComponents = 2 * N + 1 <= 8;
 
@@ -559,16 +565,21 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
     // (labels: the lowest body of each component, 4-bit fields of `lab`, merged per pair hit).
     uint64_t cslots = 0;
     if constexpr (kSolveComponents<N>) {
-        uint32_t lab = 0;
-        uint64_t osp = 0;  // byte k: the record slots whose first body is k
+        constexpr int FW = kSlotBits<N>;                  // slot-mask field width
+        constexpr uint32_t FM = (1u << FW) - 1u;
+        using LabT = std::conditional_t<(S::Nb <= 8), uint32_t, uint64_t>;
+        constexpr LabT ONES = (LabT)0x1111111111111111ull, SEVENS = (LabT)0x7777777777777777ull,
+                       EIGHTS = (LabT)0x8888888888888888ull;
+        LabT lab = 0;
+        uint64_t osp = 0;  // field k: the record slots whose first body is k
         int r = 0;
         sfor<S::Nb>([&](auto K) {  // body k's segment records: slots [r, r + count)
             constexpr int k = K;
             const uint32_t bits = (uint32_t)(hsw[k / BPW] >> (kNSeg * (k % BPW))) & 0xfffu;
             const int cnt = __popc(bits);
-            const uint32_t rng = r < 8 ? (((1u << (cnt < 8 ? cnt : 8)) - 1u) << r) & 0xffu : 0u;
-            osp |= (uint64_t)rng << (8 * k);
-            lab |= (uint32_t)k << (4 * k);
+            const uint32_t rng = r < FW ? (((1u << (cnt < FW ? cnt : FW)) - 1u) << r) & FM : 0u;
+            osp |= (uint64_t)rng << (FW * k);
+            lab |= (LabT)k << (4 * k);
             r += cnt;
         });
         sfor<NPW>([&](auto Q) {
@@ -582,20 +593,20 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
                     i += q >= k * S::Nb - k * (k + 1) / 2 ? 1 : 0;
                 });
                 const int j = q - (i * S::Nb - i * (i + 1) / 2) + i + 1;
-                osp |= (uint64_t)(r < 8 ? 1u << r : 0u) << (8 * i);
+                osp |= (uint64_t)(r < FW ? 1u << r : 0u) << (FW * i);
                 ++r;
                 // union: every field labelled max(ci, cj) becomes min(ci, cj) (SWAR zero-field test)
-                const uint32_t ci = (lab >> (4 * i)) & 15u, cj = (lab >> (4 * j)) & 15u;
-                const uint32_t lo = ci < cj ? ci : cj, hi = ci < cj ? cj : ci;
-                const uint32_t x = lab ^ (hi * 0x11111111u);
-                const uint32_t z = ~(((x & 0x77777777u) + 0x77777777u) | x) & 0x88888888u;
-                const uint32_t fm = (z >> 3) * 15u;
-                lab = (lab & ~fm) | ((lo * 0x11111111u) & fm);
+                const LabT ci = (lab >> (4 * i)) & 15u, cj = (lab >> (4 * j)) & 15u;
+                const LabT lo = ci < cj ? ci : cj, hi = ci < cj ? cj : ci;
+                const LabT x = lab ^ (hi * ONES);
+                const LabT z = ~(((x & SEVENS) + SEVENS) | x) & EIGHTS;
+                const LabT fm = (z >> 3) * 15u;
+                lab = (lab & ~fm) | ((lo * ONES) & fm);
             }
         });
         sfor<S::Nb>([&](auto K) {
             constexpr int k = K;
-            cslots |= ((osp >> (8 * k)) & 0xffu) << (8 * ((lab >> (4 * k)) & 15u));
+            cslots |= ((osp >> (FW * k)) & FM) << (FW * (uint32_t)((lab >> (4 * k)) & 15u));
         });
     }
 
@@ -856,14 +867,20 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
         uint64_t cm = whole;
         uint32_t cbase = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
         int total = __popcll(act);
+        constexpr int FW = kSlotBits<N>;
+        constexpr int NFLD = kSolveComponents<N> ? (FW == 8 ? 8 : S::Nb) : 1;  // slot-mask fields
         if constexpr (kSolveComponents<N>) {
             const uint64_t cc = n > KL ? whole : cslots;
-            // nonzero bytes of cc (components of this env), then their wave prefix
-            const uint64_t nzb = ((cc | ((cc & 0x7f7f7f7f7f7f7f7full) + 0x7f7f7f7f7f7f7f7full)) >> 7) & 0x0101010101010101ull;
+            // nonzero fields of cc (components of this env), then their wave prefix
+            uint64_t nzb;
+            if constexpr (FW == 8)
+                nzb = ((cc | ((cc & 0x7f7f7f7f7f7f7f7full) + 0x7f7f7f7f7f7f7f7full)) >> 7) & 0x0101010101010101ull;
+            else
+                nzb = ((cc | ((cc & 0x7777777777777777ull) + 0x7777777777777777ull)) >> 3) & 0x1111111111111111ull;
             const int nc = __popcll(nzb);
             uint32_t cb = 0, ct = 0;
 #pragma unroll
-            for (int b = 0; b < 4; ++b) {  // nc <= 8
+            for (int b = 0; b < 5; ++b) {  // nc <= 16
                 const uint64_t mb = __ballot((nc >> b) & 1);
                 cb += __builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, 0u)) << b;
                 ct += (uint32_t)__popcll(mb) << b;
@@ -877,8 +894,8 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
         // the wave's longest item (records): m
         int msz = 0;
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            const int c = __popc((uint32_t)(cm >> (8 * b)) & 0xffu);
+        for (int b = 0; b < NFLD; ++b) {
+            const int c = __popc((uint32_t)(cm >> (FW * b)) & ((1u << FW) - 1u));
             msz = c > msz ? c : msz;
         }
         int m = 0;
@@ -905,8 +922,8 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
                 const uint32_t tail = (uint32_t)ln | ((uint32_t)pc << 14) | ((uint32_t)(n < 65535 ? n : 65535) << 16);
                 int idx = 0;
 #pragma unroll
-                for (int b = 0; b < (kSolveComponents<N> ? 8 : 1); ++b) {
-                    const uint32_t byte = (uint32_t)(cm >> (8 * b)) & 0xffu;
+                for (int b = 0; b < NFLD; ++b) {
+                    const uint32_t byte = (uint32_t)(cm >> (FW * b)) & ((1u << FW) - 1u);
                     const uint32_t slot = byte ? cbase + (uint32_t)idx : (uint32_t)EPW;
                     sh->item[slot] = tail | (byte << 6);
                     idx += byte ? 1 : 0;
