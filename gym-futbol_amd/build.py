@@ -30,10 +30,16 @@ CFLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-ffp-contract=off", "-
 # default (4) leaves the fp64 arms of the action / contact code as divergent branches (~40 cycles
 # each on a wave64); 20 measured best for the 2v2 step (-1.5% step time).  Only for the N <= 3
 # instances: the 5v5 float instance built this way (~500 VGPRs, spills) corrupted its step
-# counter on the GPU (tests/test_gpu_api.py episode lengths), so N >= 5 and v0 keep the default.
+# counter on the GPU (tests/test_gpu_api.py episode lengths), so N >= 5 keeps the default.
 PHI = os.environ.get("FUTBOL_PHI_FOLD", "20")
-PHI_FLAGS = ["-mllvm", "-two-entry-phi-node-folding-threshold=" + PHI, "-mllvm", "-phi-node-folding-threshold=" + PHI]
-PHI_SOURCES = ("futbol_v1_n1_e64.hip", "futbol_v1_n2_e64.hip", "futbol_v1_n3_e64.hip")
+PHI_SOURCES = {"futbol_v1_n1_e64.hip": PHI, "futbol_v1_n2_e64.hip": PHI, "futbol_v1_n3_e64.hip": PHI,
+               "futbol_v0.hip": os.environ.get("FUTBOL_PHI_FOLD_V0", "50")}  # v0: 50 measured best (-1.9%)
+
+
+def _phi_flags(src):
+    t = PHI_SOURCES.get(os.path.basename(src))
+    return [] if t is None else ["-mllvm", "-two-entry-phi-node-folding-threshold=" + t,
+                                 "-mllvm", "-phi-node-folding-threshold=" + t]
 # A/B of compiler options: FUTBOL_EXTRA_CFLAGS="..." (with a FUTBOL_BUILD_VARIANT name)
 CFLAGS += os.environ.get("FUTBOL_EXTRA_CFLAGS", "").split()
 if VARIANT == "stamps":
@@ -58,7 +64,7 @@ def _stale(target, sources):
 def _compile(src, force):
     obj = os.path.join(OBJ, os.path.basename(src) + ".o")
     if force or _stale(obj, [src] + _deps()):
-        cmd = [HIPCC] + CFLAGS + (PHI_FLAGS if os.path.basename(src) in PHI_SOURCES else []) + ["-c", src, "-o", obj]
+        cmd = [HIPCC] + CFLAGS + _phi_flags(src) + ["-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("hipcc failed for %s:\n%s\n%s" % (src, " ".join(cmd), r.stderr[-8000:]))
