@@ -634,38 +634,55 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
     };
     // the contact and record of hit `pid` of env column o (env id oenv), record slot r
     auto contact = [&](int o, int oenv, int pid, int r, bool attach) {
-        double nx, ny, p1x, p1y, p2x, p2y, apx, apy, avx, avy, bpx = 0.0, bpy = 0.0, bvx_ = 0.0, bvy_ = 0.0, nMass, ee;
-        int a, bcode;
-        if (pid < S::Nb * kNSeg) {  // circle (body a) - segment sg: b is the static body
-            a = pid / kNSeg;
-            const int sg = pid - a * kNSeg;
-            const double2 pa = sh_->vb(a, o), va = sh_->v(a, o);
-            const bool ball = a == S::BALL;
-            constexpr double nmB = 1.0 / (kBallMinv + 0.0), nmP = 1.0 / (kPlayerMinv + 0.0);
-            cs_contact(pa.x, pa.y, ball ? kBallR : kPlayerR, sh_->seg[sg], nx, ny, p1x, p1y, p2x, p2y);
-            apx = pa.x; apy = pa.y; avx = va.x; avy = va.y;
-            nMass = ball ? nmB : nmP;
-            ee = kE * 0.0;
-            bcode = 32 + sg;
-        } else {  // circle pair (a, b), a < b: a is a player (the ball is the last body)
-            const int q = pid - S::Nb * kNSeg;
-            int i = 0;
-            sfor<1, S::Nb - 1>([&](auto K) {
-                constexpr int k = K;
-                i += q >= k * S::Nb - k * (k + 1) / 2 ? 1 : 0;
-            });
-            const int j = q - (i * S::Nb - i * (i + 1) / 2) + i + 1;
-            const double2 pa = sh_->vb(i, o), va = sh_->v(i, o), pb = sh_->vb(j, o), vb = sh_->v(j, o);
-            const bool ball_j = j == S::BALL;
-            constexpr double nmB = 1.0 / (kPlayerMinv + kBallMinv), nmP = 1.0 / (kPlayerMinv + kPlayerMinv);
-            cc_contact(pa.x, pa.y, kPlayerR, pb.x, pb.y, ball_j ? kBallR : kPlayerR, nx, ny, p1x, p1y, p2x, p2y);
-            apx = pa.x; apy = pa.y; avx = va.x; avy = va.y;
-            bpx = pb.x; bpy = pb.y; bvx_ = vb.x; bvy_ = vb.y;
-            nMass = ball_j ? nmB : nmP;
-            ee = kE * kE;
-            a = i;
-            bcode = j;
+        // CircleToSegment (circle a, segment sg: the second body is the static one) and
+        // CircleToCircle (pair a < j: a is a player, the ball is the last body) share one
+        // expression chain from the circle's centre to the other point -- the segment's closest
+        // point q with radius 1, or body j's centre with its radius -- so every lane of the work
+        // list runs one sqrt, one division and one preStep whatever the type of its contact
+        const bool segc = pid < S::Nb * kNSeg;
+        const int q = pid - S::Nb * kNSeg;
+        int i = 0;
+        sfor<1, S::Nb - 1>([&](auto K) {
+            constexpr int k = K;
+            i += q >= k * S::Nb - k * (k + 1) / 2 ? 1 : 0;
+        });
+        const int as = pid / kNSeg;
+        const int a = segc ? as : i;
+        const int sg = segc ? pid - as * kNSeg : 0;
+        const int j = segc ? a : q - (i * S::Nb - i * (i + 1) / 2) + i + 1;  // (segment: any valid row)
+        const double2 pa = sh_->vb(a, o), va = sh_->v(a, o), pb = sh_->vb(j, o), vbj = sh_->v(j, o);
+        const SegLds g = sh_->seg[sg];
+        double qx, qy;
+        seg_closest(pa.x, pa.y, g.ax, g.ay, g.sdx, g.sdy, g.L2, g.rL2, qx, qy);
+        const bool ball_a = a == S::BALL, ball_j = j == S::BALL;
+        const double ra = ball_a ? kBallR : kPlayerR;
+        const double rb = segc ? kSegR : (ball_j ? kBallR : kPlayerR);
+        const double ox = segc ? qx : pb.x, oy = segc ? qy : pb.y;
+        const double dx = ox - pa.x, dy = oy - pa.y;
+        const double d = sqrt(dx * dx + dy * dy);
+        double nx, ny;
+        if (d != 0.0) {
+            const double inv = 1.0 / d;
+            nx = dx * inv;
+            ny = dy * inv;
+        } else if (segc) {  // segment->tn
+            const double inv = 1.0 / sqrt(g.L2);
+            nx = -g.sdy * inv;
+            ny = g.sdx * inv;
+        } else {
+            nx = 1.0;
+            ny = 0.0;
         }
+        const double p1x = pa.x + nx * ra, p1y = pa.y + ny * ra;
+        const double p2x = ox + nx * (-rb), p2y = oy + ny * (-rb);
+        const double apx = pa.x, apy = pa.y, avx = va.x, avy = va.y;
+        const double bpx = segc ? 0.0 : pb.x, bpy = segc ? 0.0 : pb.y;   // the static body's p = (0, 0)
+        const double bvx_ = segc ? 0.0 : vbj.x, bvy_ = segc ? 0.0 : vbj.y;
+        constexpr double nmSB = 1.0 / (kBallMinv + 0.0), nmSP = 1.0 / (kPlayerMinv + 0.0);
+        constexpr double nmCB = 1.0 / (kPlayerMinv + kBallMinv), nmCP = 1.0 / (kPlayerMinv + kPlayerMinv);
+        const double nMass = segc ? (ball_a ? nmSB : nmSP) : (ball_j ? nmCB : nmCP);
+        const double ee = segc ? kE * 0.0 : kE * kE;
+        const int bcode = segc ? 32 + sg : j;
         // cpArbiterUpdate + preStep (needs the pre-damping v)
         const double r1x = p1x - apx, r1y = p1y - apy;
         const double r2x = p2x - bpx, r2y = p2y - bpy;
