@@ -434,7 +434,8 @@ __device__ __forceinline__ void load_cache_pre(const Lane<N, EPW>& L, uint32_t n
 // ck / cj: the preloaded cache entries (load_cache_pre) of the env's CURRENT cache
 template <int N, int EPW>
 __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>& L, Env<N>& e, int dtc,
-                                           const uint32_t (&ck)[CKN<N>], const double (&cj)[CKN<N>]
+                                           const uint32_t (&ck)[CKN<N>], const double (&cj)[CKN<N>],
+                                           bool& goal, bool& pre_aged
 #ifdef FUTBOL_STAMPS
                                            , unsigned long long* st_stamps, unsigned long long& _stamp_prev
 #endif
@@ -462,6 +463,12 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
         e.bx[k] = 0.0;
         e.by[k] = 0.0;
     });
+    // ball_contact_goal (envs_v1/futbol_env.py:291-296) of the step's space.step(0.1): the positions
+    // are final here (the solve changes velocities only); the caller scores with it
+    goal = false;
+    if (dtc == 2 && !far_from_segments(e.px[S::BALL], e.py[S::BALL], 2.0, W, H)) {
+        for (int s = 6; s < 12; ++s) goal = goal || cs_hit(P, s, e.px[S::BALL], e.py[S::BALL], kBallR);
+    }
 
     FUTBOL_CRUMB(L, 10 + dtc);
     FUTBOL_STAMP(dtc == 2 ? 16 : 9);
@@ -1071,15 +1078,26 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
 
     FUTBOL_CRUMB(L, 60 + dtc);
     FUTBOL_STAMP(dtc == 2 ? 6 : 9);
-    // cpSpaceArbiterSetFilter + store jnAcc: survivors (untouched, age+1 < 3) then this step's contacts
+    // cpSpaceArbiterSetFilter + store jnAcc: survivors (untouched, age+1 < 3) then this step's contacts.
+    // A lane that scored will restart from formation with the contact-free micro-step
+    // (formation_step: its guard is decided by this step's final v_bias), whose only effect on
+    // the cache is one more filter with no contact: it is applied here (ages + 1 more, survivors
+    // age + 2 < 3), so that the restart does not read the cache back
+    bool fok = goal;
+    sfor<S::Nb>([&](auto K) {
+        constexpr int k = K;
+        fok = fok && __builtin_fabs(e.bx[k]) < P.form_vb && __builtin_fabs(e.by[k]) < P.form_vb;
+    });
+    pre_aged = fok;
+    const uint32_t xa = fok ? 1u : 0u;
     uint32_t w = 0;
 #pragma unroll
     for (int c = 0; c < CKN<N>; ++c) {
         if ((uint32_t)c < ncache) {
             const uint32_t key = ck[c], age = key >> 12;
-            if (!((touched >> c) & 1u) && age + 1 < 3) {
+            if (!((touched >> c) & 1u) && age + 1 + xa < 3) {
                 FB_BOUND(L, w < (uint32_t)S::P, 6, w = S::P - 1);
-                L.ckey[(size_t)w * B + env] = (uint16_t)((key & 0x3ffu) | ((age + 1) << 12));
+                L.ckey[(size_t)w * B + env] = (uint16_t)((key & 0x3ffu) | ((age + 1 + xa) << 12));
                 FB_BOUND(L, w < (uint32_t)S::P, 6, w = S::P - 1);
                 L.cjn[(size_t)w * B + env] = cj[c];
                 ++w;
@@ -1104,11 +1122,11 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
                 const uint32_t age = key[i] >> 12;
                 bool t = false;
                 for (int s = 0; s < n; ++s) t |= ((L.get_info(s) >> 11) & 511) == pair;
-                if (!t && age + 1 < 3) {
+                if (!t && age + 1 + xa < 3) {
                     FB_BOUND(L, w < (uint32_t)S::P, 6, w = S::P - 1);
                     L.cjn[(size_t)w * B + env] = jn[i];
                     FB_BOUND(L, w < (uint32_t)S::P, 6, w = S::P - 1);
-                    L.ckey[(size_t)w * B + env] = (uint16_t)(pair | ((age + 1) << 12));
+                    L.ckey[(size_t)w * B + env] = (uint16_t)(pair | ((age + 1 + xa) << 12));
                     ++w;
                 }
             }
@@ -1116,7 +1134,7 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
     }
     for (int s = 0; s < n; ++s) {
         FB_BOUND(L, w < (uint32_t)S::P, 6, w = S::P - 1);
-        L.ckey[(size_t)w * B + env] = (uint16_t)((L.get_info(s) >> 11) & 511);
+        L.ckey[(size_t)w * B + env] = (uint16_t)(((L.get_info(s) >> 11) & 511) | (xa << 12));
         FB_BOUND(L, w < (uint32_t)S::P, 6, w = S::P - 1);
         L.cjn[(size_t)w * B + env] = L.get_jn(s);
         ++w;
@@ -1136,7 +1154,8 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
 // runs on whichever lanes need it (a goal lane's restart costs a few hundred cycles instead of a
 // whole narrowphase).
 template <int N, int EPW>
-__device__ __forceinline__ bool formation_step(const V1Params& P, const Lane<N, EPW>& L, Env<N>& e)
+__device__ __forceinline__ bool formation_step(const V1Params& P, const Lane<N, EPW>& L, Env<N>& e,
+                                               bool cache_done = false)
 {
     using S = V1Shape<N>;
     bool ok = true;
@@ -1156,6 +1175,7 @@ __device__ __forceinline__ bool formation_step(const V1Params& P, const Lane<N, 
         e.vy[k] = e.vy[k] * damping + 0.0 * dt;
     });
     e.meta.set_dtcode(1);
+    if (cache_done) return true;  // the previous step's cache update already applied this filter
     // cpSpaceArbiterSetFilter with no contact: survivors keep their order, age + 1 < 3
     const uint32_t ncache = e.meta.ncache();
     const int B = L.B, env = L.env;
@@ -1302,7 +1322,8 @@ __device__ __forceinline__ void do_reset(const V1Params& P, const V1Params* __re
     uint32_t ck[CKN<N>];
     double cj[CKN<N>];
     load_cache_pre<N, EPW>(L, e.meta.ncache(), ck, cj);
-    space_step<N, EPW>(P, L, e, 1, ck, cj
+    bool goal_, pre_;
+    space_step<N, EPW>(P, L, e, 1, ck, cj, goal_, pre_
 #ifdef FUTBOL_STAMPS
                   , st_stamps, _stamp_prev
 #endif
@@ -1578,7 +1599,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
     //   phase 1: _position_to_initial after a goal, step(1e-4) (:474, :129-144)
     //   phase 2: DummyVecEnv auto-reset -> reset(), step(1e-4) (:146-150)
     double r = 0.0, ret = 0.0;
-    bool goal = false, done = false;
+    bool goal = false, done = false, pre_aged = false;
 #pragma unroll 1
     for (int ph = 0; ph < 3; ++ph) {
         if (ph == 1 && !goal) continue;
@@ -1597,14 +1618,17 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
             position_to_initial<N>(P, e);
         }
         FUTBOL_STAMP(ph == 0 ? 3 : 9);
-        // the restart micro-steps: the per-lane no-contact path unless a v_bias is huge
-        if (ph == 0 || !formation_step<N, EPW>(P, L, e)) {
+        // the restart micro-steps: the per-lane no-contact path unless a v_bias is huge (after a
+        // goal, phase 0 has already filtered the cache for it when its guard holds)
+        if (ph == 0 || !formation_step<N, EPW>(P, L, e, ph == 1 && pre_aged)) {
             if (ph != 0) load_cache_pre<N, EPW>(L, e.meta.ncache(), ck, cj);  // the cache the previous phase left behind
-            space_step<N, EPW>(P, L, e, ph == 0 ? 2 : 1, ck, cj
+            bool goal_ph;
+            space_step<N, EPW>(P, L, e, ph == 0 ? 2 : 1, ck, cj, goal_ph, pre_aged
 #ifdef FUTBOL_STAMPS
                           , st_stamps, _stamp_prev
 #endif
             );
+            if (ph == 0) goal = goal_ph;
         }
         if (ph == 0) {
             if (!out) {  // get_team_reward + get_ball_reward (:493-515)
@@ -1626,10 +1650,8 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
                 const double ix_ = bix - gx, iy_ = biy - gy;
                 r = r + (sqrt(ix_ * ix_ + iy_ * iy_) - sqrt(ax_ * ax_ + ay_ * ay_)) * 10;
             }
-            // ball_contact_goal (:291-296); a goal restarts from formation, the episode goes on
-            if (!far_from_segments(e.px[BL], e.py[BL], 2.0, W, H)) {
-                for (int s = 6; s < 12; ++s) goal = goal || cs_hit(P, s, e.px[BL], e.py[BL], kBallR);
-            }
+            // ball_contact_goal (:291-296), tested by space_step on the final positions; a goal
+            // restarts from formation, the episode goes on
             if (goal) r = r + (e.px[BL] > W - 2 ? 1000.0 : -1000.0);
             FUTBOL_STAT(31, __popcll(__ballot(goal)));
             // current_time += 0.1; done = current_time > total_time
