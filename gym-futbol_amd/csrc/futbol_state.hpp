@@ -60,7 +60,7 @@ struct V1Ptrs {
     double* cjn;
     double* stat_ret;
     uint32_t* stat_cnt;
-    double* spill;        // contact records beyond the LDS capacity: [P][8][B]
+    double* spill;        // contact records beyond the LDS capacity: [B][P - K][8]
     unsigned long long* invalid;  // count of clamped out-of-range actions
     unsigned long long* stamps;   // diagnostic builds only (FUTBOL_STAMPS): [blocks][16] cycle sums
 };

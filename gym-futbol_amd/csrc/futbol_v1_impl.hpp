@@ -203,7 +203,8 @@ __device__ __forceinline__ long long null_info()
 }
 
 // global spill record (slot s >= K): 8 doubles [nx, ny, nMass, info, bias, -bounce, jBias, jnAcc]
-// (the LDS record's four double2 in order), at spill[(s - K) * 8 + f][env]
+// (the LDS record's four double2 in order), at spill[env][s - K][f]: a record is one 64-byte line,
+// so the solve's per-sweep re-reads of an item's spill records stay in a few cache lines
 template <int N, int EPW>
 struct Lane {
     using S = V1Shape<N>;
@@ -224,7 +225,7 @@ struct Lane {
     {
         int t = s - KL;
         FB_BOUND(*this, t >= 0 && t < S::P - KL, 0, t = 0);
-        return spill + ((size_t)t * 8 + f) * B + env;
+        return spill + ((size_t)env * (S::P - KL) + t) * 8 + f;
     }
     // record s as 4 double2 (any slot)
     __device__ __forceinline__ double2 get(int s, int q) const
@@ -719,15 +720,11 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
             sh_->rec[r][2][o] = q2;
             sh_->rec[r][3][o] = q3;
         } else {
-            double* sp0 = L.spill + (size_t)(r - KLs) * 8 * B + oenv;
-            sp0[0 * (size_t)B] = q0.x;
-            sp0[1 * (size_t)B] = q0.y;
-            sp0[2 * (size_t)B] = q1.x;
-            sp0[3 * (size_t)B] = q1.y;
-            sp0[4 * (size_t)B] = q2.x;
-            sp0[5 * (size_t)B] = q2.y;
-            sp0[6 * (size_t)B] = q3.x;
-            sp0[7 * (size_t)B] = q3.y;
+            double2* sp0 = (double2*)(L.spill + ((size_t)oenv * (S::P - KLs) + (r - KLs)) * 8);
+            sp0[0] = q0;
+            sp0[1] = q1;
+            sp0[2] = q2;
+            sp0[3] = q3;
         }
     };
     n = nh;
@@ -981,7 +978,7 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
                     auto spp = [&](int s, int f) {
                         int t = s - KL;
                         FB_BOUND(L, t >= 0 && t < S::P - KL, 0, t = 0);
-                        return L.spill + ((size_t)t * 8 + f) * B + ienv;
+                        return L.spill + ((size_t)ienv * (S::P - KL) + t) * 8 + f;
                     };
                     const int nie = spill ? (int)(ent >> 16) : 0;  // env ie's record count
                     // the item's LDS records in registers for the whole solve (m is wave-uniform: the
