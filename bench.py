@@ -345,6 +345,10 @@ def main():
             stream.wait_stream(s)
     D.barrier(dev)
     torch.cuda.synchronize(dev)
+    dbg = os.environ.get("FUTBOL_BENCH_DEBUG") and graphs is not None
+    if dbg:
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record(streams[0])
     t0 = time.perf_counter()
     done_steps = 0
     ci = 0
@@ -371,9 +375,14 @@ def main():
                 stream.wait_stream(s)
             stats_buf.copy_(all_stats())
             D.reduce_episode_stats(stats_buf)  # RCCL over xGMI: [sum return, episodes, env-steps]
+    if dbg:
+        ev1.record(streams[0])
     torch.cuda.synchronize(dev)
     D.barrier(dev)
     elapsed = D.max_over_ranks(time.perf_counter() - t0, dev)
+    if dbg:
+        print("debug: wall %.1f us, events on the replay stream %.1f us" % (elapsed * 1e6, ev0.elapsed_time(ev1) * 1e3),
+              file=sys.stderr, flush=True)
     stats = D.reduce_episode_stats(all_stats().clone()).cpu().numpy()
 
     total_env_steps = B * args.steps * world
