@@ -504,23 +504,22 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
             // every segment's cpBB lies within 1 of the field border: exact reject of all 12
             const bool interior = cl > 1.0 && cr < W - 1.0 && cb > 1.0 && ct < H - 1.0;
             const BBT& T = P.bbt;
-            const bool r1 = cl <= T.r1, rW1 = cl <= T.rW1, rm1 = cl <= T.rm1, rW3 = cl <= T.rW3;
-            const bool lm1 = T.lm1 <= cr, lW1 = T.lW1 <= cr, lm3 = T.lm3 <= cr, lWp1 = T.lWp1 <= cr;
-            const bool tlo = cb <= T.tlo, tH = cb <= T.tH, t1 = cb <= T.t1, thi = cb <= T.thi;
-            const bool bm1 = T.bm1 <= ct, bhi = T.bhi <= ct, bH = T.bH <= ct, blo = T.blo <= ct;
-            uint32_t c = 0;
-            c |= (r1 && lm1 && tlo && bm1) ? 1u << 0 : 0u;
-            c |= (r1 && lm1 && tH && bhi) ? 1u << 1 : 0u;
-            c |= (rW1 && lm1 && tH && bH) ? 1u << 2 : 0u;
-            c |= (rW1 && lW1 && tlo && bm1) ? 1u << 3 : 0u;
-            c |= (rW1 && lW1 && tH && bhi) ? 1u << 4 : 0u;
-            c |= (rW1 && lm1 && t1 && bm1) ? 1u << 5 : 0u;
-            c |= (rm1 && lm3 && thi && blo) ? 1u << 6 : 0u;
-            c |= (r1 && lm3 && tlo && blo) ? 1u << 7 : 0u;
-            c |= (r1 && lm3 && thi && bhi) ? 1u << 8 : 0u;
-            c |= (rW3 && lWp1 && thi && blo) ? 1u << 9 : 0u;
-            c |= (rW3 && lW1 && tlo && blo) ? 1u << 10 : 0u;
-            c |= (rW3 && lW1 && thi && bhi) ? 1u << 11 : 0u;
+            // each of the 16 distinct bounds contributes the set of segments whose cpBB uses it;
+            // a segment is a candidate when all four of its bounds hold (the AND of four sets):
+            //   segment:  0  1  2  3  4  5  6  7  8  9 10 11
+            //   right:   r1 r1 W1 W1 W1 W1 m1 r1 r1 W3 W3 W3   (cl <= r)
+            //   left:    m1 m1 m1 W1 W1 m1 m3 m3 m3 Wp W1 W1   (l <= cr)
+            //   top:     lo  H  H lo  H  1 hi lo hi hi lo hi   (cb <= t)
+            //   bottom:  m1 hi  H m1 hi m1 lo lo hi lo lo hi   (b <= ct)
+            const uint32_t xr = (cl <= T.r1 ? 0x183u : 0u) | (cl <= T.rW1 ? 0x03cu : 0u) |
+                                (cl <= T.rm1 ? 0x040u : 0u) | (cl <= T.rW3 ? 0xe00u : 0u);
+            const uint32_t xl = (T.lm1 <= cr ? 0x027u : 0u) | (T.lW1 <= cr ? 0xc18u : 0u) |
+                                (T.lm3 <= cr ? 0x1c0u : 0u) | (T.lWp1 <= cr ? 0x200u : 0u);
+            const uint32_t yt = (cb <= T.tlo ? 0x489u : 0u) | (cb <= T.tH ? 0x016u : 0u) |
+                                (cb <= T.t1 ? 0x020u : 0u) | (cb <= T.thi ? 0xb40u : 0u);
+            const uint32_t yb = (T.bm1 <= ct ? 0x029u : 0u) | (T.bhi <= ct ? 0x912u : 0u) |
+                                (T.bH <= ct ? 0x004u : 0u) | (T.blo <= ct ? 0x6c0u : 0u);
+            const uint32_t c = xr & xl & yt & yb;
             cand |= interior ? 0ull : (uint64_t)c << (kNSeg * (i - i0));
         });
         uint64_t hitm = 0;
