@@ -58,6 +58,14 @@ constexpr int CKN = N >= 5 ? FUTBOL_CK_LARGE : FUTBOL_CK_SMALL;
 // entries beyond CKN read per batch of independent loads (5v5 and up: registers are exhausted)
 template <int N>
 constexpr int CBN = N >= 5 ? 1 : 4;
+// spill records (slots past the LDS ones) an item of the split solve holds in registers for its
+// 10 sweeps: read from the global spill area once, written back once.  Only the 5v5 instance spills
+// often (13% of its waves; 2v2 almost never); records past these still go through the global loop.
+#ifndef FUTBOL_SPILL_REGS
+#define FUTBOL_SPILL_REGS 4
+#endif
+template <int N>
+constexpr int KXN = N == 5 ? FUTBOL_SPILL_REGS : 0;
 
 // Diagnostic build only (-DFUTBOL_STAMPS, bench.py --stamps): per-wave s_memtime at phase
 // boundaries, accumulated into st.stamps[wave][slot] (kStampStride slots per wave: 0-10 phases,
@@ -1016,13 +1024,62 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
                             qslot[q] = has ? sl : -1;
                         }
                     });
+                    // the first KX spill records in registers too (wave-uniform count mx; past the
+                    // item's own records, null applications on Z with zero operands)
+                    constexpr int KX = KXN<N>;
+                    constexpr int KXa = KX > 0 ? KX : 1;
+                    double xnx[KXa], xny[KXa], xnm[KXa], xc[KXa], xacc[KXa], xma[KXa], xmb[KXa];
+                    double2 *xra[KXa], *xrb[KXa];
+                    bool xwarm[KXa], xhas[KXa];
+                    int mx = 0;
+                    if constexpr (KX > 0) {
+                        if (spill) {
+                            const int nsx = nie > KL ? (nie - KL < KX ? nie - KL : KX) : 0;
+#pragma unroll
+                            for (int b = 2; b >= 0; --b) {
+                                const int t = mx | (1 << b);
+                                if (t <= KX && __ballot(nsx >= t)) mx = t;
+                            }
+                            sfor<KX>([&](auto X) {
+                                constexpr int x = X;
+                                if (x < mx) {
+                                    const bool has = x < nsx;
+                                    // a lane without this record reads its env's first spill line (in
+                                    // bounds) and discards it
+                                    const double2* sp = (const double2*)spp(has ? KL + x : KL, 0);
+                                    const double2 d0 = sp[0], d1 = sp[1], d2 = sp[2], d3 = sp[3];
+                                    const unsigned long long info = info_of(d1.y);
+                                    uint32_t ao, bo;
+                                    info_rows<N, EPW>(info, ao, bo);
+                                    xhas[x] = has;
+                                    xra[x] = row(has ? ao : (uint32_t)S::Nb * ROW);
+                                    xrb[x] = row(has ? bo : (uint32_t)S::Nb * ROW);
+                                    xma[x] = has ? mass(ao) : 0.0;
+                                    xmb[x] = has ? mass(bo) : 0.0;
+                                    xnx[x] = has ? d0.x : 0.0;
+                                    xny[x] = has ? d0.y : 0.0;
+                                    xnm[x] = has ? d1.x : 0.0;
+                                    xc[x] = has ? (h ? d2.y : d2.x) : 0.0;
+                                    xacc[x] = has ? (h ? d3.y : d3.x) : 0.0;
+                                    xwarm[x] = has && h && ((info >> 20) & 1);
+                                }
+                            });
+                        }
+                    }
+                    const int sx0 = KL + mx;  // first spill slot the global loops handle
                     // warm start (cpArbiterApplyCachedImpulse), v half only, record order
                     sfor<KL>([&](auto Q) {
                         constexpr int q = Q;
                         if (q < m && qwarm[q]) warm_half(qra[q], qrb[q], qnx[q], qny[q], qacc[q], dt_coef, qma[q], qmb[q]);
                     });
+                    if constexpr (KX > 0) {
+                        sfor<KX>([&](auto X) {
+                            constexpr int x = X;
+                            if (x < mx && xwarm[x]) warm_half(xra[x], xrb[x], xnx[x], xny[x], xacc[x], dt_coef, xma[x], xmb[x]);
+                        });
+                    }
                     if (h) {
-                        for (int s = KL; s < nie; ++s) {
+                        for (int s = sx0; s < nie; ++s) {
                             const unsigned long long info = info_of(*spp(s, 3));
                             if ((info >> 20) & 1) {
                                 uint32_t ao, bo;
@@ -1037,7 +1094,13 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
                             constexpr int q = Q;
                             if (q < m) apply_half(qra[q], qrb[q], qnx[q], qny[q], qnm[q], qc[q], qma[q], qmb[q], qacc[q]);
                         });
-                        for (int s = KL; s < nie; ++s) {
+                        if constexpr (KX > 0) {
+                            sfor<KX>([&](auto X) {
+                                constexpr int x = X;
+                                if (x < mx) apply_half(xra[x], xrb[x], xnx[x], xny[x], xnm[x], xc[x], xma[x], xmb[x], xacc[x]);
+                            });
+                        }
+                        for (int s = sx0; s < nie; ++s) {
                             const unsigned long long info = info_of(*spp(s, 3));
                             uint32_t ao, bo;
                             info_rows<N, EPW>(info, ao, bo);
@@ -1055,6 +1118,12 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
                             else sh->rec[qslot[q]][3][ie].x = qacc[q];
                         }
                     });
+                    if constexpr (KX > 0) {
+                        sfor<KX>([&](auto X) {  // and into the spill lines
+                            constexpr int x = X;
+                            if (x < mx && xhas[x]) *spp(KL + x, 6 + h) = xacc[x];
+                        });
+                    }
                 }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
