@@ -67,7 +67,7 @@ def cpu_baseline(kind, n, budget_s=12.0, B=65536):
     dt = time.perf_counter() - t0
     return {"value": steps * B / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
             "sample": "oracle/liboracle.so (C restatement of the %s step), 1 thread, %d envs x %d steps (%.1f s)"
-                      % ("envs_v1 2v2" if kind == "v1" else "v0 hard-coded-opponent", B, steps, dt)}
+                      % ("envs_v1 %dv%d" % (n, n) if kind == "v1" else "v0 hard-coded-opponent", B, steps, dt)}
 
 
 def pmc_traffic(kind, n, B):

@@ -59,13 +59,17 @@ constexpr int CKN = N >= 5 ? FUTBOL_CK_LARGE : FUTBOL_CK_SMALL;
 template <int N>
 constexpr int CBN = N >= 5 ? 1 : 4;
 // spill records (slots past the LDS ones) an item of the split solve holds in registers for its
-// 10 sweeps: read from the global spill area once, written back once.  Only the 5v5 instance spills
-// often (13% of its waves; 2v2 almost never); records past these still go through the global loop.
+// 10 sweeps: read from the global spill area once, written back once.  The 5v5 instance spills on
+// 13% of its waves (4 measured best: 2 / 6 slower), 10v10 (2 LDS slots) on most (2 best, 4 neutral);
+// 2v2 almost never.  Records past these still go through the global loop.
 #ifndef FUTBOL_SPILL_REGS
 #define FUTBOL_SPILL_REGS 4
 #endif
+#ifndef FUTBOL_SPILL_REGS10
+#define FUTBOL_SPILL_REGS10 2
+#endif
 template <int N>
-constexpr int KXN = N == 5 ? FUTBOL_SPILL_REGS : 0;
+constexpr int KXN = N == 5 ? FUTBOL_SPILL_REGS : (N >= 10 ? FUTBOL_SPILL_REGS10 : 0);
 
 // Diagnostic build only (-DFUTBOL_STAMPS, bench.py --stamps): per-wave s_memtime at phase
 // boundaries, accumulated into st.stamps[wave][slot] (kStampStride slots per wave: 0-10 phases,
