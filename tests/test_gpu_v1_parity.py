@@ -129,10 +129,16 @@ def test_teacher_forced_crowded_states(n, B):
     v1_state_to_oracle(venv.get_state(), ora.envs, n, B)
     ex0, _, _ = v1_dense_cache(venv.get_state(), n, B)
     assert ex0.sum(1).max() > (8 if n >= 5 else 6), "some env must hold more cache entries than are preloaded"
+    # contact records per env: past the LDS slots (K = 7 / 4 / 2 for N = 2 / 5 / 10) the solve holds
+    # the first spill records in registers (0 / 4 / 2 of them) and re-reads the rest from the global
+    # spill area in every sweep -- every one of these paths must run
+    lds_slots, reg_spill = {2: 7, 5: 4, 10: 2}[n], {2: 0, 5: 4, 10: 2}[n]
+    most = 0
     for t in range(3):
         a = venv.random_actions(900 + t, seed=4321)
         obs, rew, done, _ = venv.step(a)
         o2, r2, d2, _ = ora.step(a.cpu().numpy().astype(np.int32))
+        most = max(most, max(int(np.sum(np.asarray(e.arb_inlist))) for e in ora.envs))
         assert np.array_equal(done.cpu().numpy(), d2)
         assert np.array_equal(rew.cpu().numpy(), r2), "step %d reward max diff %g" % (
             t, np.abs(rew.cpu().numpy() - r2).max())
@@ -141,6 +147,7 @@ def test_teacher_forced_crowded_states(n, B):
         _compare_state(venv, ora, n, B, "crowded step %d" % t)
     ex, _, _ = v1_dense_cache(venv.get_state(), n, B)
     assert ex.sum(1).max() > 8, "crowded states must overflow the LDS contact slots"
+    assert most > lds_slots + reg_spill, "some env must have records past the register-held spill slots"
     venv.close()
 
 
