@@ -5,7 +5,7 @@
 # Then: python scripts/pmc_traffic.py --prof gpurun_out/prof --round rNN  (CPU side)
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-OUT=$R/gpurun_out/prof
+OUT=$R/gpurun_out/${PROF_DIR:-prof}
 mkdir -p $OUT
 hipcc --offload-arch=gfx950 -O3 -o $OUT/pmc_calib $R/scripts/pmc_calib.hip || exit 1
 cd /tmp && export TMPDIR=/tmp
