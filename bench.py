@@ -47,27 +47,52 @@ def algo_bytes_per_env_step(kind, n, out_bytes):
     return 2 * (25 * 8 + 14) + 1 + 30 * out_bytes + out_bytes + 1
 
 
-def cpu_baseline(kind, n, budget_s=12.0, B=65536):
-    """Oracle (faithful build, 1 thread) on a bounded sample of the same workload."""
+def cpu_threads():
+    """The host threads this process may use: OMP_NUM_THREADS (16 on the GPU box, its CPU share
+    per GPU) or the affinity mask, at most 16."""
+    try:
+        t = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        t = 0
+    if t <= 0:
+        t = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return max(1, min(16, t))
+
+
+def cpu_baseline(kind, n, budget_s=10.0, B=65536):
+    """Oracle (faithful build) on a bounded sample of the same workload: envs split over the
+    host's threads with OpenMP (the restatement on all host cores), and 1 thread."""
     from oracle import oracle as O
-    if kind == "v1":
-        ora = O.V1Vec(B, N=n, seed=0)
-        nact, adim = 5, 2 * n
+
+    def timed(nthreads):
+        if kind == "v1":
+            ora = O.V1Vec(B, N=n, seed=0)
+            nact, adim = 5, 2 * n
+        else:
+            ora = O.V0Vec(B, seed=0, random_opp=False)
+            nact, adim = 16, 1
+        ora.reset()
+        rng = np.random.default_rng(1234)
+        steps = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < budget_s:
+            a = rng.integers(0, nact, (B, adim)).astype(np.int32)
+            ora.step(a if kind == "v1" else a.reshape(-1), nthreads=nthreads)
+            steps += 1
+        dt = time.perf_counter() - t0
+        return steps * B / dt, steps, dt
+
+    what = "envs_v1 %dv%d" % (n, n) if kind == "v1" else "v0 hard-coded-opponent"
+    T = cpu_threads()
+    v1t, s1, d1 = timed(1)
+    if T > 1:
+        vT, sT, dT = timed(T)
     else:
-        ora = O.V0Vec(B, seed=0, random_opp=False)
-        nact, adim = 16, 1
-    ora.reset()
-    rng = np.random.default_rng(1234)
-    steps = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < budget_s:
-        a = rng.integers(0, nact, (B, adim)).astype(np.int32)
-        ora.step(a if kind == "v1" else a.reshape(-1), nthreads=1)
-        steps += 1
-    dt = time.perf_counter() - t0
-    return {"value": steps * B / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": "oracle/liboracle.so (C restatement of the %s step), 1 thread, %d envs x %d steps (%.1f s)"
-                      % ("envs_v1 %dv%d" % (n, n) if kind == "v1" else "v0 hard-coded-opponent", B, steps, dt)}
+        vT, sT, dT = v1t, s1, d1
+    return {"value": vT, "unit": "env-steps/s", "cores": T, "kind": "port",
+            "sample": "oracle/liboracle.so (C restatement of the %s step), %d OpenMP threads, %d envs x %d steps "
+                      "(%.1f s); 1 thread: %d steps (%.1f s)" % (what, T, B, sT, dT, s1, d1),
+            "single_thread_value": v1t}
 
 
 def pmc_traffic(kind, n, B):
