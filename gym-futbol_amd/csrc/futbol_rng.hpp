@@ -69,6 +69,8 @@ struct Stream {
         for (int i = 0; i < n; ++i) b[i] = philox4x32_10(j + (uint32_t)i, event, env, tag, k0, k1);
     }
     __host__ __device__ inline void skip(uint32_t n) { j += n; }
+    // the block of draw index pos of this stream (absolute, consumed or not)
+    __host__ __device__ inline Philox4 block(uint32_t pos) const { return philox4x32_10(pos, event, env, tag, k0, k1); }
 
     __host__ __device__ static inline double uniform01_of(const Philox4& p) { return u53(p.x[0], p.x[1]); }
     // random.choice over n items / gym MultiDiscrete.sample for one component

@@ -35,7 +35,7 @@ struct Env {
     // a shot whose direction is still to be computed (resolve_shot): at most one agent holds the
     // ball when it shoots, so the transcendental part runs once per step, not once per agent
     bool shot;
-    Philox4 shot_p;
+    uint32_t shot_pos;  // the draw index of the shot's normal (screw_vec), drawn by resolve_shot
     double shot_cs, shot_sn, shot_mag, shot_acc;
 };
 
@@ -95,11 +95,12 @@ __device__ __forceinline__ void set_vector_observation(const Ctx& c, Env& e, boo
     const V0Params* P = c.P;
     double* ag = e.r[a];
     double* ball = e.r[BALL];
-    // every path draws target_y first and then at most three more (shoot): the blocks are
-    // computed here, where the wave is converged, and each exclusive branch takes its draws by
-    // position -- one Philox per draw position instead of one per draw site.  The fourth
-    // (shoot's randint(0, 9)) only advances the counter: its value is never used
-    Philox4 blk[3];
+    // every path draws target_y first and then at most three more (shoot): the first two blocks
+    // are computed here, where the wave is converged, and each exclusive branch takes its draws by
+    // position -- one Philox per draw position instead of one per draw site.  The third (shoot's
+    // normal) is computed by resolve_shot, once per step; the fourth (shoot's randint(0, 9)) only
+    // advances the counter: its value is never used
+    Philox4 blk[2];
     c.rs->lookahead(blk);
     uint32_t used = 1;
     const double target_y = (double)Stream::randint_of(blk[0], P->ty_lo, P->ty_hi);
@@ -133,7 +134,7 @@ __device__ __forceinline__ void set_vector_observation(const Ctx& c, Env& e, boo
             const double mag = get_vec(right ? 0.0 : P->length, target_y, ball[0], ball[1], vx, vy);
             // screw_vec (:101-116): one normal draw, then randint(0, 9) for the index; the
             // rotation (Box-Muller, sin/cos) is applied by resolve_shot before the ball moves
-            e.shot_p = blk[2];
+            e.shot_pos = c.rs->j + 2u;
             e.shot_acc = (double)acc;
             e.shot_cs = vx * 1.0 / mag;
             e.shot_sn = vy * 1.0 / mag;
@@ -184,9 +185,12 @@ __device__ __forceinline__ void set_vector_observation(const Ctx& c, Env& e, boo
     c.rs->skip(used);
 }
 
-// Easy_Agent.get_action_type (easy_agent.py:53-98), shoot_range = 20 (futbol_env.py:196-201)
+// Easy_Agent.get_action_type (easy_agent.py:53-98), shoot_range = 20 (futbol_env.py:196-201).
+// ub: the block of the stream's current draw, computed once for both opponents by opp_team (at
+// most one of them holds the ball, so at most one draws, and at that position)
 template <int a>
-__device__ __forceinline__ int get_action_type(const Ctx& c, const Env& e, bool has_ball, bool team_has_ball)
+__device__ __forceinline__ int get_action_type(const Ctx& c, const Env& e, bool has_ball, bool team_has_ball,
+                                               const Philox4& ub)
 {
     constexpr bool right = a >= 2;
     const double* ag = e.r[a];
@@ -198,8 +202,10 @@ __device__ __forceinline__ int get_action_type(const Ctx& c, const Env& e, bool 
     const double shoot_x = right ? 0.0 + 20 : c.P->length - 20;
     if (has_ball) {
         if ((right && ag[0] <= shoot_x) || (!right && ag[0] >= shoot_x)) return SHOOT;
-        if ((mate[0] < ag[0] || mate[1] < ag[1] - 7 || mate[1] > ag[1] + 7) && c.rs->uniform01() > 0.8 && mtam > 12)
-            return ASSIST;
+        if (mate[0] < ag[0] || mate[1] < ag[1] - 7 || mate[1] > ag[1] + 7) {  // random() drawn only then
+            c.rs->skip(1);
+            if (Stream::uniform01_of(ub) > 0.8 && mtam > 12) return ASSIST;
+        }
         return RUN;
     }
     if (btam <= 1 && !team_has_ball) return INTERCEPT;
@@ -221,10 +227,10 @@ __device__ __forceinline__ void step_by_observation(double* o)
 // the ball's _step_by_observation reads the ball's direction -- later agents either leave it or
 // overwrite it (which cancels the pending shot), and the opponents' ball anticipation only runs
 // when neither opponent's action was SHOOT
-__device__ __forceinline__ void resolve_shot(Env& e)
+__device__ __forceinline__ void resolve_shot(Env& e, const Stream& rs)
 {
     if (!e.shot) return;
-    const double nd = Stream::normal_of(e.shot_p, 0.0, e.shot_acc);
+    const double nd = Stream::normal_of(rs.block(e.shot_pos), 0.0, e.shot_acc);
     const double ang = (nd / 180) * 3.141592653589793;
     double ss, sc;
     cr_sincos(ang, &ss, &sc);
@@ -241,8 +247,9 @@ __device__ __forceinline__ void opp_team(const Ctx& c, Env& e)
     const V0Params* P = c.P;
     const bool o1has = e.owner == OPP_1, o2has = e.owner == OPP_2;
     const bool team = o1has || o2has;
-    int a1 = get_action_type<OPP_1>(c, e, o1has, team);
-    int a2 = get_action_type<OPP_2>(c, e, o2has, team);
+    const Philox4 ub = c.rs->block(c.rs->j);
+    int a1 = get_action_type<OPP_1>(c, e, o1has, team, ub);
+    int a2 = get_action_type<OPP_2>(c, e, o2has, team, ub);
     const int opp1_action = a1, opp2_action = a2;  // the Action enums keep the pre-override values (D.13)
     bool s1 = false, s2 = false;
     double t1x = 0, t1y = 0, t2x = 0, t2y = 0;
@@ -468,7 +475,7 @@ __global__ void __launch_bounds__(64) v0_step_kernel(const V0Params* __restrict_
     }
     set_vector_observation<AI_1>(c, e, e.owner == AI_1, a0, false, 0, 0);
     set_vector_observation<AI_2>(c, e, e.owner == AI_2, a1, false, 0, 0);
-    resolve_shot(e);
+    resolve_shot(e, rs);
 #pragma unroll
     for (int r = 0; r < 5; ++r) step_by_observation(e.r[r]);
 
