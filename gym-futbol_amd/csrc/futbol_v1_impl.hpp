@@ -68,8 +68,11 @@ constexpr int CBN = N >= 5 ? 1 : 4;
 #ifndef FUTBOL_SPILL_REGS10
 #define FUTBOL_SPILL_REGS10 2
 #endif
+#ifndef FUTBOL_SPILL_REGS2
+#define FUTBOL_SPILL_REGS2 0
+#endif
 template <int N>
-constexpr int KXN = N == 5 ? FUTBOL_SPILL_REGS : (N >= 10 ? FUTBOL_SPILL_REGS10 : 0);
+constexpr int KXN = N == 5 ? FUTBOL_SPILL_REGS : (N >= 10 ? FUTBOL_SPILL_REGS10 : (N == 2 ? FUTBOL_SPILL_REGS2 : 0));
 
 // Diagnostic build only (-DFUTBOL_STAMPS, bench.py --stamps): per-wave s_memtime at phase
 // boundaries, accumulated into st.stamps[wave][slot] (kStampStride slots per wave: 0-10 phases,
@@ -135,6 +138,9 @@ constexpr int kSlotBits = 2 * N + 1 <= 8 ? 8 : 4;
 template <int N>
 constexpr bool kSolveComponents = 2 * N + 1 <= 8;
 
+#ifndef FUTBOL_K2
+#define FUTBOL_K2 7
+#endif
 template <int N>
 struct V1Shape {
     static constexpr int Nb = 2 * N + 1;
@@ -142,7 +148,7 @@ struct V1Shape {
     static constexpr int P = v1_npairs(N);
     // LDS contact-record slots per lane: 4 one-wave blocks per CU must fit in 160 KB
     // (40 KB per block: K * 4 KB of records + (2 Nb + 1) KB of solver velocity rows + the segment table)
-    static constexpr int K = N == 1 ? 8 : (N == 2 ? 7 : (N == 3 ? 6 : (N == 5 ? 4 : 2)));
+    static constexpr int K = N == 1 ? 8 : (N == 2 ? FUTBOL_K2 : (N == 3 ? 6 : (N == 5 ? 4 : 2)));
 };
 
 __device__ __forceinline__ double minv_of(int k, int ball) { return k == ball ? kBallMinv : kPlayerMinv; }
