@@ -1,0 +1,47 @@
+"""CPU checks of bench.py's reporting helpers (the GPU timing itself runs only on the box):
+the algorithmic bytes per env-step of SURVEY.md 8(d), the committed PMC traffic lookup, and the
+cpu_baseline record (the oracle on the host's threads and on one thread)."""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "gym-futbol_amd")]
+import bench  # noqa: E402
+
+
+def test_algorithmic_bytes_match_survey():
+    # 579 B (2v2), 1 257 B (5v5) per envs_v1 env-step, 554 B per v0 env-step,
+    # with float32 observations
+    assert bench.algo_bytes_per_env_step("v1", 2, 4) == 579
+    assert bench.algo_bytes_per_env_step("v1", 5, 4) == 1257
+    assert bench.algo_bytes_per_env_step("v0", 2, 4) == 554
+
+
+@pytest.mark.parametrize("n", [2, 5])
+def test_committed_traffic_entry(n):
+    traffic, src = bench.pmc_traffic("v1", n, 65536)
+    assert src is not None and src.startswith("profiles/")
+    algo = bench.algo_bytes_per_env_step("v1", n, 4) * 65536
+    # measured HBM bytes per launch: at least the algorithmic ones (the arbiter cache and spill
+    # area come on top), and not wildly more
+    assert algo <= traffic < 1.5 * algo
+
+
+def test_cpu_threads_bounds(monkeypatch):
+    monkeypatch.setenv("OMP_NUM_THREADS", "64")
+    assert bench.cpu_threads() == 16
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    assert bench.cpu_threads() == 3
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    assert 1 <= bench.cpu_threads() <= 16
+
+
+@pytest.mark.parametrize("kind", ["v1", "v0"])
+def test_cpu_baseline_record(kind, monkeypatch):
+    monkeypatch.setenv("OMP_NUM_THREADS", "2")
+    r = bench.cpu_baseline(kind, 2, budget_s=0.2, B=256)
+    assert r["unit"] == "env-steps/s" and r["kind"] == "port" and r["cores"] == 2
+    assert r["value"] > 0 and r["single_thread_value"] > 0
+    assert "2 OpenMP threads" in r["sample"] and "1 thread" in r["sample"]
