@@ -37,6 +37,65 @@ import torch  # noqa: E402
 
 METRIC = "env-steps/sec (whole node), 2v2 Futbol, batch=65536 envs, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
+# reference v0 FutbolEnv.step() timed by the survey (not this box): envs_v1 cannot
+# run here (pymunk absent), so these are the only numbers of the reference's own code
+REF_V0_PYTHON = {"random_opp_env_steps_per_s_1core": 14188, "hardcoded_opp_env_steps_per_s_1core": 12372,
+                 "hardcoded_opp_env_steps_per_s_8proc": 65746,
+                 "where": "survey container, 8 cores 'Intel(R) Xeon(R) Processor', Python 3.10 / numpy 2.2 "
+                          "(SURVEY.md 6), not the GPU box"}
+
+
+def metric_of(kind, n, B):
+    """BASELINE.json's metric for its own configs (C2/C4 2v2 is the headline); the other kinds get a
+    label of their own so that a C3 / C5 line is never read as the 2v2 metric."""
+    if kind == "v1" and n == 2 and B == 65536:
+        return METRIC
+    if kind == "v1":
+        return "env-steps/sec (whole node), %dv%d Futbol, batch=%d envs, MI355X" % (n, n, B)
+    return "env-steps/sec (whole node), 2v2 Futbol-v0 with the hard-coded opponent, batch=%d envs, MI355X" % B
+
+
+def workload_of(kind, n, B, world):
+    if kind == "v0":
+        return "C3: %d envs/GPU v0 FutbolEnv(random_opp=False), hard-coded opponent on the GPU" % B
+    tag = {2: "C4" if world > 1 else "C2", 5: "C5"}.get(n, "envs_v1 %dv%d (not a BASELINE config)" % (n, n))
+    return "%s: %d envs/GPU envs_v1 %dv%d, synthetic random actions, auto-reset" % (tag, B, n, n)
+
+
+def host_cpu():
+    """CPU model and thread counts of this host (cpu_baseline context)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": aff}
+
+
+def c1_baseline(n=2, steps=100000):
+    """1 env, 1 thread, 100 000 steps, state seed 0, left actions from the synthetic
+    Philox stream (seed 1234), auto-reset -- the oracle (C restatement) in a C loop: the reference's own
+    envs_v1 step needs pymunk, absent here."""
+    import ctypes as C
+    from oracle import oracle as O
+    L = O.lib()
+    e = O.OrcV1()
+    L.orc_v1_init(C.byref(e), n, 105.0, 68.0, 30.0, 0, 0)
+    obs = np.zeros(4 * (2 * n + 1))
+    L.orc_v1_reset(C.byref(e), obs.ctypes.data)
+    ret = C.c_double()
+    t0 = time.perf_counter()
+    eps = L.orc_v1_run(C.byref(e), steps, 1234, C.byref(ret))
+    dt = time.perf_counter() - t0
+    return {"value": steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port", "envs": 1, "steps": steps,
+            "seconds": dt, "episodes": eps, "mean_return": ret.value / max(eps, 1),
+            "sample": "C1: oracle/liboracle.so orc_v1_run, 1 env %dv%d, 1 thread, %d steps, seed 0, Philox(1234) "
+                      "left actions, auto-reset" % (n, n, steps)}
 
 
 def algo_bytes_per_env_step(kind, n, out_bytes):
@@ -89,10 +148,38 @@ def cpu_baseline(kind, n, budget_s=10.0, B=65536):
         vT, sT, dT = timed(T)
     else:
         vT, sT, dT = v1t, s1, d1
-    return {"value": vT, "unit": "env-steps/s", "cores": T, "kind": "port",
-            "sample": "oracle/liboracle.so (C restatement of the %s step), %d OpenMP threads, %d envs x %d steps "
-                      "(%.1f s); 1 thread: %d steps (%.1f s)" % (what, T, B, sT, dT, s1, d1),
-            "single_thread_value": v1t}
+    out = {"value": vT, "unit": "env-steps/s", "cores": T, "kind": "port",
+           "sample": "oracle/liboracle.so (C restatement of the %s step), %d OpenMP threads, %d envs x %d steps "
+                     "(%.1f s); 1 thread: %d steps (%.1f s)" % (what, T, B, sT, dT, s1, d1),
+           "single_thread_value": v1t, "host": host_cpu(), "reference_v0_python": REF_V0_PYTHON}
+    if kind == "v1" and n == 2:
+        out["c1"] = c1_baseline(n)
+    return out
+
+
+def copy_ceiling(dev, mib=1024, reps=10):
+    """Measured HBM stream-copy ceiling (SURVEY 8(d) Roofline): futbol_stream_copy of a `mib` MiB
+    buffer (16 B per lane), HIP events on the launch stream; GB/s = 2 x bytes / time."""
+    from gym_futbol_amd import _native as nat
+    nbytes = mib << 20
+    src = torch.empty(nbytes, dtype=torch.uint8, device=dev).fill_(1)
+    dst = torch.empty_like(src)
+    stream = torch.cuda.current_stream(dev)
+    lib = nat.load()
+    for _ in range(2):
+        nat.check(lib.futbol_stream_copy(src.data_ptr(), dst.data_ptr(), nbytes, stream.cuda_stream))
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        nat.check(lib.futbol_stream_copy(src.data_ptr(), dst.data_ptr(), nbytes, stream.cuda_stream))
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    ok = bool(torch.equal(src[:4096], dst[:4096]))
+    del src, dst
+    return {"gbs": 2 * nbytes / (ms * 1e-3) / 1e9, "bytes_copied": nbytes, "ms_per_copy": ms, "verified": ok,
+            "method": "futbol_stream_copy (16 B/lane, 4 loads in flight per lane), %d MiB, %d reps, HIP events"
+                      % (mib, reps)}
 
 
 def pmc_traffic(kind, n, B):
@@ -184,7 +271,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--players", type=int, default=2)
-    ap.add_argument("--kind", default="v1", choices=["v1", "v0"])
+    ap.add_argument("--kind", default="v1", choices=["v1", "v0", "c1"],
+                    help="v1: envs_v1 (C2/C4, --players 5: C5); v0: hard-coded opponent (C3); c1: the C1 CPU line")
     ap.add_argument("--graph", type=int, default=1, help="replay the timed steps from a hipGraph")
     ap.add_argument("--groups", type=int, default=1,
                     help="step the B envs as this many independent env groups (B/groups envs each: one "
@@ -202,6 +290,16 @@ def main():
     ap.add_argument("--stamps", action="store_true",
                     help="diagnostic: load the FUTBOL_STAMPS build and print the per-phase cycle breakdown")
     args = ap.parse_args()
+    if args.kind == "c1":  # 1 env on 1 CPU thread, no GPU
+        c1 = c1_baseline(args.players)
+        print(json.dumps({"metric": "env-steps/sec, 1 env %dv%d envs_v1 step, 1 CPU thread (C1)"
+                          % (args.players, args.players), "value": c1["value"], "unit": "env-steps/s",
+                          "n_gpus": 0, "steps": c1["steps"], "warmup": 0, "ms_per_step": 1e3 / c1["value"],
+                          "higher_is_better": True, "scaling": None, "vs_baseline": None, "dtype": "f64",
+                          "data": "synthetic", "config": {"workload": c1["sample"]}, "host": host_cpu(),
+                          "episodes": c1["episodes"], "mean_return": c1["mean_return"],
+                          "reference_v0_python": REF_V0_PYTHON}), flush=True)
+        return
     if args.stamps:
         os.environ["FUTBOL_LIB_VARIANT"] = "stamps"
 
@@ -326,7 +424,9 @@ def main():
                 for _ in range(args.warmup + 2 * args.profile_steps):
                     ge.random_actions(ALL, seed=1234, out=ge._act)
                     ge.step_raw(ge._act)
-            abuf = torch.empty((args.steps, ge.num_envs, ge.action_dim), dtype=torch.uint8, device=dev)
+            # zeros (valid noop actions) until the timed region's fill: the untimed warm replay below
+            # steps on them, and must not feed uninitialised bytes to the kernel
+            abuf = torch.zeros((args.steps, ge.num_envs, ge.action_dim), dtype=torch.uint8, device=dev)
             graphs.append(([capture(ge, s, abuf, t0_, n_) for t0_, n_ in chunks], abuf))
         # one untimed replay of each graph: the first launch of a graph pays its upload
         for (gl, abuf), s in zip(graphs, streams):
@@ -363,11 +463,18 @@ def main():
     stats_buf = torch.zeros(3, dtype=torch.float64, device=dev)
     for ge in groups:
         ge.episode_stats(clear=True)
+    fill_ms = None
     if graphs is not None:  # the synthetic inputs of the K timed steps, fresh draws, into HBM
+        f0, f1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        f0.record(stream)
         for ge, (gl, abuf), s in zip(groups, graphs, streams):
+            s.wait_stream(stream)
             with torch.cuda.stream(s):
                 ge.random_actions_steps(args.steps, ALL, seed=1234, out=abuf)
             stream.wait_stream(s)
+        f1.record(stream)
+        torch.cuda.synchronize(dev)
+        fill_ms = f0.elapsed_time(f1) / args.steps
     D.barrier(dev)
     torch.cuda.synchronize(dev)
     dbg = os.environ.get("FUTBOL_BENCH_DEBUG") and graphs is not None
@@ -416,13 +523,20 @@ def main():
     per_env = algo_bytes_per_env_step(args.kind, n, out_bytes)
     achieved = per_env * B / (kernel_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(args.kind, n, B)
+    ndev = D.distinct_devices(dev)
+    ceil = copy_ceiling(dev) if rank == 0 else None
     line = {
-        "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+        "metric": metric_of(args.kind, n, B), "value": value, "unit": "env-steps/s", "n_gpus": ndev,
+        "ranks": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-        "config": {"workload": ("C2/C4: %d envs/GPU envs_v1 %dv%d, synthetic random actions, auto-reset"
-                                % (B, n, n)) if args.kind == "v1" else
-                   ("C3: %d envs/GPU v0 FutbolEnv, hard-coded opponent" % B),
+        "config": {"workload": workload_of(args.kind, n, B, world),
+                   "actions": ("synthetic Philox left-team actions of all %d timed steps drawn on the GPU by one "
+                               "fill launch before the timed region (resident in HBM, not timed; the fill costs "
+                               "action_fill_ms_per_step); the opponent's actions are drawn inside the step kernel"
+                               % args.steps) if graphs is not None else
+                              "synthetic Philox left-team actions drawn by a fill launch before every step (timed)",
+                   "action_fill_ms_per_step": fill_ms,
                    "episode_phases": "staggered" if args.stagger else "lockstep (DummyVecEnv)",
                    "timed_from_episode_step": None if args.stagger else
                    (args.warmup + 2 * args.profile_steps + (args.steps if graphs is not None else 0) + align)
@@ -431,6 +545,9 @@ def main():
                    "obs_dtype": "f32", "hip_graph": bool(graphs is not None), "env_groups": ngroups},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "copy_ceiling_gbs": ceil["gbs"] if ceil else None,
+                     "frac_of_copy_ceiling": achieved / ceil["gbs"] if ceil else None,
+                     "copy_ceiling": ceil,
                      "kernel": "v1_step_kernel<%d,float>" % n if args.kind == "v1" else "v0_step_kernel<float>",
                      "kernel_ms": kernel_ms, "kernel_ms_dispatch_events": kernel_ms_dispatch,
                      "kernel_timing": "HIP events around a hipGraph of %d back-to-back step launches"

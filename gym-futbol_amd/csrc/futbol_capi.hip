@@ -203,7 +203,7 @@ extern "C" int futbol_create(const FutbolConfig* cfg, int32_t device, uint64_t s
         return fail(nullptr, FUTBOL_EINVAL, "global env ids must fit in 32 bits");
     if (cfg->out_dtype != FUTBOL_F32 && cfg->out_dtype != FUTBOL_F64) return fail(nullptr, FUTBOL_EINVAL, "out_dtype");
     if (cfg->env_kind == FUTBOL_ENV_V1 && !v1_supported(cfg->number_of_player))
-        return fail(nullptr, FUTBOL_EUNSUPPORTED, "number_of_player must be one of 1,2,3,5,10");
+        return fail(nullptr, FUTBOL_EUNSUPPORTED, "number_of_player must be 1..10 (team.py:52-112)");
     if (cfg->env_kind != FUTBOL_ENV_V1 && cfg->env_kind != FUTBOL_ENV_V0)
         return fail(nullptr, FUTBOL_EINVAL, "env_kind");
 
@@ -571,4 +571,10 @@ extern "C" int futbol_debug_stamps(FutbolCtx* ctx, uint64_t* host_out, int64_t n
     FB_CHECK_HIP(ctx, hipMemcpy(host_out, ctx->d_stamps, bytes, hipMemcpyDeviceToHost));
     if (clear) FB_CHECK_HIP(ctx, hipMemset(ctx->d_stamps, 0, bytes));
     return FUTBOL_OK;
+}
+
+extern "C" int futbol_stream_copy(const void* src, void* dst, uint64_t bytes, void* stream)
+{
+    if (!src || !dst || (bytes & 15u)) return fail(nullptr, FUTBOL_EINVAL, "stream_copy: null buffer or bytes % 16");
+    return launch_stream_copy(src, dst, (size_t)bytes, (hipStream_t)stream) == 0 ? FUTBOL_OK : FUTBOL_EHIP;
 }

@@ -91,6 +91,7 @@ int launch_fill_actions(uint64_t seed, uint64_t step, unsigned long long* step_c
                         int adim, int nvals, uint8_t* actions, hipStream_t stream);
 int launch_fill_actions_steps(uint64_t seed, uint64_t step0, int nsteps, unsigned long long* ctr, uint32_t env_base,
                               int B, int adim, int nvals, uint8_t* actions, hipStream_t stream);
+int launch_stream_copy(const void* src, void* dst, size_t bytes, hipStream_t stream);
 int launch_episode_stats(const double* stat_ret, const uint32_t* stat_cnt, int B, double steps, double* out3,
                          int clear, double* stat_ret_w, uint32_t* stat_cnt_w, hipStream_t stream);
 

@@ -121,4 +121,31 @@ int launch_episode_stats(const double* stat_ret, const uint32_t* stat_cnt, int B
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// HBM copy ceiling (measurement only: bench.py's roofline.copy_ceiling_gbs, SURVEY 8(d) "a measured
+// stream-copy ceiling"): 16 bytes per lane, four independent loads in flight per lane, then four
+// stores; blocks of 256 lanes cover 16 KB each.  bytes must be a multiple of 16.
+__global__ void __launch_bounds__(256) stream_copy_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                          size_t n)
+{
+    const size_t i0 = (size_t)blockIdx.x * 1024 + threadIdx.x;
+    uint4 a[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (i0 + (size_t)k * 256 < n) a[k] = src[i0 + (size_t)k * 256];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (i0 + (size_t)k * 256 < n) dst[i0 + (size_t)k * 256] = a[k];
+}
+
+int launch_stream_copy(const void* src, void* dst, size_t bytes, hipStream_t stream)
+{
+    const size_t n = bytes / 16;
+    const size_t blocks = (n + 1023) / 1024;
+    if (blocks == 0) return 0;
+    if (blocks > 0x7fffffffull) return -1;
+    hipLaunchKernelGGL(stream_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, (const uint4*)src, (uint4*)dst,
+                       n);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 }  // namespace futbol

@@ -12,7 +12,12 @@ namespace futbol {
 FUTBOL_DECL(1)
 FUTBOL_DECL(2)
 FUTBOL_DECL(3)
+FUTBOL_DECL(4)
 FUTBOL_DECL(5)
+FUTBOL_DECL(6)
+FUTBOL_DECL(7)
+FUTBOL_DECL(8)
+FUTBOL_DECL(9)
 FUTBOL_DECL(10)
 #undef FUTBOL_DECL
 
@@ -22,11 +27,12 @@ int launch_v1(int N, int epw, int def, const V1Params* P, int B, const V1Ptrs& s
 {
     if (epw != 64) return -2;
     switch (N) {
-    case 1: return launch_v1_n1_e64(P, B, st, out64, what, def, actions, mask, obs, reward, done, term, init, stream);
-    case 2: return launch_v1_n2_e64(P, B, st, out64, what, def, actions, mask, obs, reward, done, term, init, stream);
-    case 3: return launch_v1_n3_e64(P, B, st, out64, what, def, actions, mask, obs, reward, done, term, init, stream);
-    case 5: return launch_v1_n5_e64(P, B, st, out64, what, def, actions, mask, obs, reward, done, term, init, stream);
-    case 10: return launch_v1_n10_e64(P, B, st, out64, what, def, actions, mask, obs, reward, done, term, init, stream);
+#define FUTBOL_CASE(n)                                                                                    \
+    case n:                                                                                               \
+        return launch_v1_n##n##_e64(P, B, st, out64, what, def, actions, mask, obs, reward, done, term, init, stream);
+    FUTBOL_CASE(1) FUTBOL_CASE(2) FUTBOL_CASE(3) FUTBOL_CASE(4) FUTBOL_CASE(5)
+    FUTBOL_CASE(6) FUTBOL_CASE(7) FUTBOL_CASE(8) FUTBOL_CASE(9) FUTBOL_CASE(10)
+#undef FUTBOL_CASE
     default: return -2;
     }
 }
@@ -36,11 +42,10 @@ bool v1_is_default_geometry(int N, const V1Params& p)
 {
     V1Params g{};
     switch (N) {
-    case 1: g = v1_default_geometry<1>(); break;
-    case 2: g = v1_default_geometry<2>(); break;
-    case 3: g = v1_default_geometry<3>(); break;
-    case 5: g = v1_default_geometry<5>(); break;
-    case 10: g = v1_default_geometry<10>(); break;
+#define FUTBOL_CASE(n) case n: g = v1_default_geometry<n>(); break;
+    FUTBOL_CASE(1) FUTBOL_CASE(2) FUTBOL_CASE(3) FUTBOL_CASE(4) FUTBOL_CASE(5)
+    FUTBOL_CASE(6) FUTBOL_CASE(7) FUTBOL_CASE(8) FUTBOL_CASE(9) FUTBOL_CASE(10)
+#undef FUTBOL_CASE
     default: return false;
     }
     V1Params q = p;  // runtime fields are not part of the geometry
@@ -52,18 +57,19 @@ bool v1_is_default_geometry(int N, const V1Params& p)
     return memcmp(&q, &g, sizeof(V1Params)) == 0;
 }
 
-int v1_supported(int N) { return N == 1 || N == 2 || N == 3 || N == 5 || N == 10; }
+// every number_of_player the reference's Team formation implements (team.py:52-112: N <= 10;
+// larger teams print "unimplemented" and fail)
+int v1_supported(int N) { return N >= 1 && N <= 10; }
 int v1_supported_epw(int epw) { return epw == 64; }
 
 // spill slots needed in the worst case (largest EPW = fewest LDS slots)
 size_t v1_spill_slots(int N)
 {
     switch (N) {
-    case 1: return V1Shape<1>::P - V1Shape<1>::K;
-    case 2: return V1Shape<2>::P - V1Shape<2>::K;
-    case 3: return V1Shape<3>::P - V1Shape<3>::K;
-    case 5: return V1Shape<5>::P - V1Shape<5>::K;
-    case 10: return V1Shape<10>::P - V1Shape<10>::K;
+#define FUTBOL_CASE(n) case n: return V1Shape<n>::P - V1Shape<n>::K;
+    FUTBOL_CASE(1) FUTBOL_CASE(2) FUTBOL_CASE(3) FUTBOL_CASE(4) FUTBOL_CASE(5)
+    FUTBOL_CASE(6) FUTBOL_CASE(7) FUTBOL_CASE(8) FUTBOL_CASE(9) FUTBOL_CASE(10)
+#undef FUTBOL_CASE
     default: return 0;
     }
 }

@@ -71,8 +71,9 @@ constexpr int CBN = N >= 5 ? 1 : 4;
 #ifndef FUTBOL_SPILL_REGS2
 #define FUTBOL_SPILL_REGS2 0
 #endif
+// (N = 6..9, with 1-3 LDS slots, take the 10v10 count; N = 1, 3, 4 rarely spill: none)
 template <int N>
-constexpr int KXN = N == 5 ? FUTBOL_SPILL_REGS : (N >= 10 ? FUTBOL_SPILL_REGS10 : (N == 2 ? FUTBOL_SPILL_REGS2 : 0));
+constexpr int KXN = N == 5 ? FUTBOL_SPILL_REGS : (N >= 6 ? FUTBOL_SPILL_REGS10 : (N == 2 ? FUTBOL_SPILL_REGS2 : 0));
 
 // Diagnostic build only (-DFUTBOL_STAMPS, bench.py --stamps): per-wave s_memtime at phase
 // boundaries, accumulated into st.stamps[wave][slot] (kStampStride slots per wave: 0-10 phases,
@@ -148,7 +149,9 @@ struct V1Shape {
     static constexpr int P = v1_npairs(N);
     // LDS contact-record slots per lane: 4 one-wave blocks per CU must fit in 160 KB
     // (40 KB per block: K * 4 KB of records + (2 Nb + 1) KB of solver velocity rows + the segment table)
-    static constexpr int K = N == 1 ? 8 : (N == 2 ? FUTBOL_K2 : (N == 3 ? 6 : (N == 5 ? 4 : 2)));
+    // for N <= 7; N = 8, 9, 10 (the rows alone take 35-43 KB) fit 3 blocks per CU (53 KB each)
+    static constexpr int K = N == 1 ? 8 : (N == 2 ? FUTBOL_K2 : (N == 3 ? 6 : (N == 4 ? 5 : (N == 5 ? 4 :
+                             (N == 6 ? 3 : (N == 7 ? 2 : (N == 8 ? 4 : (N == 9 ? 3 : 2))))))));
 };
 
 __device__ __forceinline__ double minv_of(int k, int ball) { return k == ball ? kBallMinv : kPlayerMinv; }
@@ -1779,6 +1782,8 @@ __global__ void __launch_bounds__(EPW) v1_step_kernel(const V1Params* __restrict
                                                       OT* __restrict__ reward, uint8_t* __restrict__ done_out,
                                                       OT* __restrict__ term_obs)
 {
+    // 4 blocks per CU (160 KB of LDS) up to N = 7, 3 blocks beyond
+    static_assert(sizeof(Scratch<N, EPW>) <= (N <= 7 ? 160 * 1024 / 4 : 160 * 1024 / 3), "LDS per block");
     __shared__ Scratch<N, EPW> sh;
     if constexpr (DEF) {
         constexpr V1Params G = v1_default_geometry<N>();

@@ -1,0 +1,3 @@
+// futbol_v1_n9_e64.hip -- the envs_v1 kernels for number_of_player = 9 (futbol_v1_inst.hpp)
+#include "futbol_v1_inst.hpp"
+FUTBOL_V1_INSTANCE(9)

@@ -57,6 +57,7 @@ SIGNATURES = [
     ("futbol_episode_limit", C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
     ("futbol_debug_stamps", C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32]),
     ("futbol_kernel_timing", C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
+    ("futbol_stream_copy", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
 ]
 
 _lib = None

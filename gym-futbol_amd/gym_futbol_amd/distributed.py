@@ -84,6 +84,23 @@ def max_over_ranks(seconds, device):
     return float(t.item())
 
 
+def distinct_devices(device):
+    """Number of distinct physical devices the ranks run on (host name + device UUID / PCI id):
+    a rehearsal that puts several ranks on one GPU reports 1, not world."""
+    import socket
+    if device.type == "cuda":
+        p = torch.cuda.get_device_properties(device)
+        ident = str(getattr(p, "uuid", "")) or "%s:%s" % (getattr(p, "pci_bus_id", ""), getattr(p, "pci_device_id", ""))
+    else:
+        ident = "cpu"
+    key = "%s/%s/%d" % (socket.gethostname(), ident, device.index if device.index is not None else -1)
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return 1
+    keys = [None] * dist.get_world_size()
+    dist.all_gather_object(keys, key)
+    return len(set(keys))
+
+
 def barrier(device):
     if dist.is_initialized() and dist.get_world_size() > 1:
         if device.type == "cuda" and dist.get_backend() == "nccl":

@@ -17,6 +17,17 @@ AI_1, AI_2, OPP_1, OPP_2, NOONE = range(5)
 RUN, INTERCEPT, SHOOT, ASSIST = range(4)
 
 
+def v0_attrs_from_state(st, i):
+    """The reference FutbolEnv's per-env attributes (envs/futbol_env.py: ball_owner, last_ball_owner,
+    time -- accumulated 0.1 per step in fp64 --, ai_score, opp_score) of env i of a host state dict."""
+    from .vec_env import _accumulated_time
+    meta = int(st["meta"][i])
+    B = st["meta"].shape[0]
+    return {"ball_owner": meta & 7, "last_ball_owner": (meta >> 3) & 7,
+            "time": _accumulated_time((meta >> 18) & 0x3FFF),
+            "ai_score": int(st["score"][i]), "opp_score": int(st["score"][B + i])}
+
+
 class FutbolEnv:
     def __init__(self, length=105, width=68, goal_size=10, game_time=40, player_speed=12, shoot_speed=20,
                  Debug=False, pressure_range=2, one_goal_end=False, action_as_int=True, only_reward_goal=False,
@@ -65,27 +76,23 @@ class FutbolEnv:
 
     @property
     def ball_owner(self):
-        return int(self._venv.get_state()["meta"][0] & np.uint64(7))
+        return v0_attrs_from_state(self._venv.get_state(), 0)["ball_owner"]
 
     @property
     def last_ball_owner(self):
-        return int((self._venv.get_state()["meta"][0] >> np.uint64(3)) & np.uint64(7))
+        return v0_attrs_from_state(self._venv.get_state(), 0)["last_ball_owner"]
 
     @property
     def time(self):
-        steps = int((self._venv.get_state()["meta"][0] >> np.uint64(18)) & np.uint64(0x3FFF))
-        t = 0
-        for _ in range(steps):
-            t += 0.1
-        return t
+        return v0_attrs_from_state(self._venv.get_state(), 0)["time"]
 
     @property
     def ai_score(self):
-        return int(self._venv.get_state()["score"][0])
+        return v0_attrs_from_state(self._venv.get_state(), 0)["ai_score"]
 
     @property
     def opp_score(self):
-        return int(self._venv.get_state()["score"][1])
+        return v0_attrs_from_state(self._venv.get_state(), 0)["opp_score"]
 
     def render(self, mode="human", close=False):
         import matplotlib.pyplot as plt

@@ -52,15 +52,13 @@ class Futbol:
     # -- attributes of the reference env --------------------------------------
     @property
     def current_time(self):
-        steps = int((self._venv.get_state()["meta"][0] >> np.uint64(18)) & np.uint64(0x3FFF))
-        t = 0
-        for _ in range(steps):
-            t += 0.1  # futbol_env.py:478 accumulates in fp64
-        return t
+        """futbol_env.py:478 accumulates 0.1 per step in fp64 (memoised sums, vec_env._accumulated_time).
+        Like the reference it keeps counting past the episode end when stepping on without reset."""
+        return self._venv.env_attr("current_time")[0]
 
     @property
     def ball_owner_side(self):
-        return "left" if int(self._venv.get_state()["meta"][0] & np.uint64(7)) == 0 else "right"
+        return self._venv.env_attr("ball_owner_side")[0]
 
     def body_states(self):
         """(positions [Nb,2], velocities [Nb,2]) of A0.., B0.., ball."""
@@ -70,24 +68,41 @@ class Futbol:
     def render(self, ax=None):
         """Matplotlib drawing of the field (replaces pymunk's debug_draw, futbol_env.py:236-243)."""
         import matplotlib.pyplot as plt
-        from matplotlib.patches import Circle
         p, _ = self.body_states()
         pad = 5
         if ax is None:
             ax = plt.axes(xlim=(0 - pad, self.width + pad), ylim=(0 - pad, self.height + pad))
         ax.set_aspect("equal")
-        n = self.number_of_player
-        w, h, g = self.width, self.height, 20
-        for (x0, y0), (x1, y1) in [((0, 0), (0, h / 2 - g / 2)), ((0, h / 2 + g / 2), (0, h)), ((0, h), (w, h)),
-                                   ((w, 0), (w, h / 2 - g / 2)), ((w, h / 2 + g / 2), (w, h)), ((0, 0), (w, 0))]:
-            ax.plot([x0, x1], [y0, y1], "k-")
-        for k in range(2 * n + 1):
-            color = "g" if k == 2 * n else ("r" if k < n else "b")
-            ax.add_patch(Circle(tuple(p[k]), 1.0 if k == 2 * n else 1.5, color=color))
+        draw_field(ax, self.width, self.height, p, self.number_of_player)
         return ax
 
     def close(self):
         self._venv.close()
+
+
+def field_segments(width, height, goal_size=20):
+    """The 12 static segments of _setup_walls (futbol_env.py:182-234): 6 walls, then the 6
+    goal-box segments behind each goal mouth ([(x0, y0), (x1, y1)], radius 1 each)."""
+    w, h, g = width, height, goal_size
+    lo, hi = h / 2 - g / 2, h / 2 + g / 2
+    walls = [((0, 0), (0, lo)), ((0, hi), (0, h)), ((0, h), (w, h)),
+             ((w, 0), (w, lo)), ((w, hi), (w, h)), ((0, 0), (w, 0))]
+    goals = [((-2, lo), (-2, hi)), ((-2, lo), (0, lo)), ((-2, hi), (0, hi)),
+             ((w + 2, lo), (w + 2, hi)), ((w, lo), (w + 2, lo)), ((w, hi), (w + 2, hi))]
+    return walls + goals
+
+
+def draw_field(ax, width, height, positions, n):
+    """Matplotlib equivalent of pymunk's space.debug_draw (futbol_env.py:236-243): the 12 segments
+    (walls black, goal boxes grey, drawn with the segments' radius 1), the 2N players (radius 1.5,
+    left red / right blue like Team's colour ramps, team.py:34-50) and the ball (radius 1)."""
+    from matplotlib.patches import Circle
+    for s, ((x0, y0), (x1, y1)) in enumerate(field_segments(width, height)):
+        ax.plot([x0, x1], [y0, y1], "-", color="k" if s < 6 else "0.5", lw=2, solid_capstyle="round")
+    for k in range(2 * n + 1):
+        color = "g" if k == 2 * n else ("r" if k < n else "b")
+        ax.add_patch(Circle(tuple(positions[k]), 1.0 if k == 2 * n else 1.5, color=color))
+    return ax
 
 
 def observation_from_state(state, n, env=0):

@@ -204,8 +204,34 @@ class FutbolVecEnv:
         return self.step(a)
 
     def seed(self, seed=None):
-        # env randomness is counter-based: re-seeding = a new context (see make())
+        """Re-seed every env (DummyVecEnv.seed: env i gets seed + i; here one context seed keys every
+        env's Philox stream by its global id).  The randomness is counter-based, so re-seeding builds
+        a new context with the same configuration: like the reference's constructor it ends in
+        reset(), so call reset() before stepping.  seed=None keeps the current seed."""
+        if seed is not None and int(seed) != self.seed_value:
+            cfg = self.ctx.cfg
+            self.ctx.close()
+            with torch.cuda.device(self.device):
+                self.ctx = nat.Context(cfg, self.device.index, int(seed), self.env_id_base, self.num_envs)
+            self.seed_value = int(seed)
         return [self.seed_value + i for i in range(self.num_envs)]
+
+    # per-env attributes of the reference envs, read from the device state
+    def env_attr(self, name):
+        """Per-env values of a reference attribute: v1 `current_time`, `ball_owner_side`; v0 `time`,
+        `ball_owner`, `last_ball_owner`, `ai_score`, `opp_score`.  None if `name` is not per-env."""
+        st = None
+        if self.kind == "v1" and name in ("current_time", "ball_owner_side"):
+            st = self.get_state()
+            meta = st["meta"].astype(np.uint64)
+            if name == "ball_owner_side":
+                return ["left" if int(m & np.uint64(7)) == 0 else "right" for m in meta]
+            return [_accumulated_time(int((m >> np.uint64(18)) & np.uint64(0x3FFF))) for m in meta]
+        if self.kind == "v0" and name in ("time", "ball_owner", "last_ball_owner", "ai_score", "opp_score"):
+            from .envs import v0_attrs_from_state
+            st = self.get_state()
+            return [v0_attrs_from_state(st, i)[name] for i in range(self.num_envs)]
+        return None
 
     def as_sb3(self):
         return SB3VecEnv(self)
@@ -215,6 +241,17 @@ class FutbolVecEnv:
             self.close()
         except Exception:
             pass
+
+
+def _accumulated_time(steps):
+    """current_time after `steps` steps: the reference accumulates 0.1 in fp64
+    (envs_v1/futbol_env.py:478); memoised running sums, no per-call loop."""
+    while len(_TIMES) <= steps:
+        _TIMES.append(_TIMES[-1] + 0.1)
+    return _TIMES[steps]
+
+
+_TIMES = [0.0]
 
 
 try:  # pragma: no cover - stable-baselines3 is not installed in this image
@@ -273,17 +310,50 @@ class SB3VecEnv(_SB3Base):
         self.venv.close()
 
     def seed(self, seed=None):
-        return self.venv.seed(seed)
+        """Re-seeds the envs (a new context, see FutbolVecEnv.seed); the next reset() starts from it."""
+        out = self.venv.seed(seed)
+        self._ep_ret[:] = 0
+        self._ep_len[:] = 0
+        return out
 
     def get_attr(self, attr_name, indices=None):
-        n = len(self._idx(indices))
-        return [getattr(self.venv, attr_name)] * n
+        """Per-env reference attributes (current_time, ball_owner_side; v0 time, scores, owners) are
+        read per env; the others are configuration shared by every env of the vector."""
+        idx = list(self._idx(indices))
+        per_env = self.venv.env_attr(attr_name)
+        if per_env is not None:
+            return [per_env[i] for i in idx]
+        return [getattr(self.venv, attr_name)] * len(idx)
 
     def set_attr(self, attr_name, value, indices=None):
+        """Attributes are shared by every env of the context: setting one for a subset of the envs
+        cannot be represented and raises."""
+        if not self._all(indices):
+            raise NotImplementedError("set_attr(%r) on a subset of the envs: the attributes of a FutbolVecEnv "
+                                      "are shared by all its envs" % attr_name)
         setattr(self.venv, attr_name, value)
 
     def env_method(self, method_name, *args, indices=None, **kwargs):
-        return [getattr(self.venv, method_name)(*args, **kwargs)] * len(self._idx(indices))
+        """Per-env methods of the reference env: `reset` (masked reset of the selected envs; returns their
+        observations) and `random_action` (one sample per env).  Any other method acts on the whole
+        vector at once, so it is only accepted for all envs and called once."""
+        idx = list(self._idx(indices))
+        if method_name == "reset":
+            mask = np.zeros(self.num_envs, np.uint8)
+            mask[idx] = 1
+            obs = self.venv.reset(mask).cpu().numpy().astype(self.observation_space.dtype)
+            self._ep_ret[idx] = 0
+            self._ep_len[idx] = 0
+            return [obs[i] for i in idx]
+        if method_name == "random_action":
+            return [self.venv.action_space.sample() for _ in idx]
+        if not self._all(indices):
+            raise NotImplementedError("env_method(%r) on a subset of the envs: only reset and random_action are "
+                                      "per-env methods of a FutbolVecEnv" % method_name)
+        return [getattr(self.venv, method_name)(*args, **kwargs)] * len(idx)
+
+    def _all(self, indices):
+        return indices is None or sorted(set(self._idx(indices))) == list(range(self.num_envs))
 
     def env_is_wrapped(self, wrapper_class, indices=None):
         return [False] * len(self._idx(indices))

@@ -144,6 +144,12 @@ int futbol_debug_stamps(FutbolCtx* ctx, uint64_t* host_out, int64_t n, int32_t c
  * the number of timed launches.  Not usable inside hipGraph capture. */
 int futbol_kernel_timing(FutbolCtx* ctx, int32_t mode, double* total_ms, int64_t* count);
 
+/* HBM copy ceiling (measurement, not part of the reference interface): copies `bytes`
+ * (a multiple of 16) from device buffer src to dst with a plain 16-byte-per-lane copy kernel
+ * on `stream`.  bench.py times it to report the achievable stream-copy bandwidth next to
+ * the 8 TB/s spec (Roofline). */
+int futbol_stream_copy(const void* src, void* dst, uint64_t bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

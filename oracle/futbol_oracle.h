@@ -87,6 +87,9 @@ void orc_v1_space_step(OrcV1 *e, double dt);
 void orc_v1_vec_step(OrcV1 *envs, int B, const int32_t *actions, double *obs, double *reward,
                      uint8_t *done, double *terminal_obs, int nthreads);
 
+/* C1: one env, nsteps steps in a C loop, synthetic Philox (tag 1) left actions, auto-reset */
+int  orc_v1_run(OrcV1 *e, int nsteps, uint64_t act_seed, double *ret_sum);
+
 void orc_v0_init(OrcV0 *e, double length, double width, double goal_size, double game_time,
                  double player_speed, double shoot_speed, int one_goal_end, int only_reward_goal,
                  int random_opp, uint64_t seed, uint32_t env_id);

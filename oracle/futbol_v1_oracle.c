@@ -577,6 +577,32 @@ void orc_v1_vec_step(OrcV1 *envs, int B, const int32_t *actions, double *obs, do
     }
 }
 
+/* one env stepped nsteps times in a C loop (no per-step Python), left-team actions
+   from the synthetic Philox stream (tag 1, key act_seed, counter (j/4, step, env id)), DummyVecEnv
+   auto-reset on done.  Returns the number of finished episodes; *ret_sum = sum of their returns
+   (so the work cannot be optimised away and the run is checkable). */
+int orc_v1_run(OrcV1 *e, int nsteps, uint64_t act_seed, double *ret_sum)
+{
+    double obs[4 * ORC_MAXB], ret = 0.0, tot = 0.0;
+    int32_t left[2 * ORC_MAXN];
+    int episodes = 0;
+    for (int t = 0; t < nsteps; ++t) {
+        OracleRng g = { act_seed, e->env_id, (uint32_t)t, 0, 1 };
+        oracle_words_choice(&g, 2 * e->N, 5, left);
+        double r;
+        const int d = orc_v1_step(e, left, obs, &r);
+        ret += r;
+        if (d) {
+            tot += ret;
+            ret = 0.0;
+            ++episodes;
+            orc_v1_reset(e, obs);
+        }
+    }
+    *ret_sum = tot;
+    return episodes;
+}
+
 void orc_philox(const uint32_t *ctr, const uint32_t *key, uint32_t *out) { oracle_philox4x32_10(ctr, key, out); }
 
 void orc_draw_u01(uint64_t seed, uint32_t env_id, uint32_t event, uint32_t j, uint32_t tag, double *u, double *z)

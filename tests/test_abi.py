@@ -65,13 +65,12 @@ def test_create_rejects_bad_arguments_without_touching_a_device(nat):
     h = C.c_void_p()
     assert lib.futbol_create(C.byref(cfg), 0, 0, 0, 0, C.byref(h)) == -1          # num_envs = 0
     assert b"num_envs" in lib.futbol_last_error(None)
-    cfg.number_of_player = 4
-    assert lib.futbol_create(C.byref(cfg), 0, 0, 0, 8, C.byref(h)) == -4          # unsupported N
+    for bad_n in (0, 11):                                                         # team.py:52-112: 1..10
+        cfg.number_of_player = bad_n
+        assert lib.futbol_create(C.byref(cfg), 0, 0, 0, 8, C.byref(h)) == -4      # unsupported N
     cfg = nat.default_config(nat.ENV_V1, 2)
     cfg.abi_version = 99
     assert lib.futbol_create(C.byref(cfg), 0, 0, 0, 8, C.byref(h)) == -1
     cfg = nat.default_config(nat.ENV_V1, 2)
     assert lib.futbol_create(C.byref(cfg), 0, 0, 2**32 - 4, 8, C.byref(h)) == -1  # env ids > 32 bits
-    for fn in ("futbol_reset", "futbol_destroy"):
-        pass
     assert lib.futbol_step(None, None, None, None, None, None, None) == -1

@@ -45,3 +45,31 @@ def test_cpu_baseline_record(kind, monkeypatch):
     assert r["unit"] == "env-steps/s" and r["kind"] == "port" and r["cores"] == 2
     assert r["value"] > 0 and r["single_thread_value"] > 0
     assert "2 OpenMP threads" in r["sample"] and "1 thread" in r["sample"]
+    assert r["host"]["nproc"] >= 1 and "reference_v0_python" in r
+    if kind == "v1":
+        c1 = r["c1"]  # 1 env, 1 thread, 100 000 steps
+        assert c1["envs"] == 1 and c1["cores"] == 1 and c1["steps"] == 100000 and c1["value"] > 0
+        assert c1["episodes"] == 100000 // 300  # fixed 300-step episodes
+
+
+def test_metric_labels_per_config():
+    # the headline metric is BASELINE.json's, and only the 2v2 envs_v1 config carries it
+    import json
+    with open(os.path.join(ROOT, "BASELINE.json")) as f:
+        assert bench.metric_of("v1", 2, 65536) == json.load(f)["metric"]
+    assert "5v5" in bench.metric_of("v1", 5, 65536) and bench.metric_of("v1", 5, 65536) != bench.METRIC
+    assert "hard-coded" in bench.metric_of("v0", 2, 65536)
+    assert bench.workload_of("v1", 2, 65536, 1).startswith("C2:")
+    assert bench.workload_of("v1", 2, 65536, 8).startswith("C4:")
+    assert bench.workload_of("v1", 5, 65536, 1).startswith("C5:")
+    assert bench.workload_of("v0", 2, 65536, 1).startswith("C3:")
+
+
+def test_c1_line():
+    import json
+    import subprocess
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--kind", "c1"], capture_output=True,
+                         text=True, timeout=300, check=True).stdout.strip().splitlines()
+    line = json.loads(out[-1])
+    assert line["n_gpus"] == 0 and line["steps"] == 100000 and line["value"] > 0
+    assert line["host"]["cpu_model"] is not None or line["host"]["nproc"] >= 1

@@ -237,6 +237,30 @@ def test_sb3_adapter():
         assert infos[i]["terminal_observation"].shape == (20,)
         assert infos[i]["episode"]["l"] == 300
     assert sb.get_attr("number_of_player") == [2] * 16
+    # per-env attributes are read per env (all 300-step episodes just auto-reset: time 0)
+    assert sb.get_attr("current_time", indices=[0, 3]) == [0.0, 0.0]
+    assert set(sb.get_attr("ball_owner_side")) <= {"left", "right"}
+    with pytest.raises(NotImplementedError):
+        sb.set_attr("number_of_player", 3, indices=[1])
+    with pytest.raises(NotImplementedError):
+        sb.env_method("close", indices=[2])
+    # env_method("reset") is a masked reset of the selected envs only
+    for t in range(5):
+        o, r, d, infos = sb.step(rng.integers(0, 5, (16, 4)))
+    before = sb.get_attr("current_time")
+    obs = sb.env_method("reset", indices=[1, 5])
+    after = sb.get_attr("current_time")
+    assert len(obs) == 2 and obs[0].shape == (20,)
+    assert after[1] == after[5] == 0.0 and after[0] == before[0] > 0.4
+    # seed(): a new context; same seed -> same trajectory, other seed -> another one
+    def roll(seed):
+        sb.seed(seed)
+        sb.reset()
+        out = [sb.step(np.zeros((16, 4), np.int64))[0] for _ in range(30)]
+        return np.stack(out)
+    a, b, c = roll(21), roll(22), roll(21)
+    assert np.array_equal(a, c) and not np.array_equal(a, b)
+    assert sb.seed(None) == [21 + i for i in range(16)]
     sb.close()
 
 

@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import (O, v1_dense_cache, v1_oracle_bodies, v1_oracle_dense_cache, v1_oracle_to_state,
+from helpers import (O, npairs, v1_dense_cache, v1_oracle_bodies, v1_oracle_dense_cache, v1_oracle_to_state,
                      v1_state_to_oracle)
 
 pytestmark = pytest.mark.gpu
@@ -42,7 +42,13 @@ def _compare_state(venv, ora, n, B, tag):
     assert np.array_equal(ev, np.array([ora.envs[i].event for i in range(B)])), tag + ": rng event"
 
 
+# LDS record slots and register-held spill slots per team size (futbol_v1_impl.hpp V1Shape / KXN)
+LDS_SLOTS = {1: 8, 2: 7, 3: 6, 4: 5, 5: 4, 6: 3, 7: 2, 8: 4, 9: 3, 10: 2}
+REG_SPILL = {1: 0, 2: 0, 3: 0, 4: 0, 5: 4, 6: 2, 7: 2, 8: 2, 9: 2, 10: 2}
+
+
 @pytest.mark.parametrize("n,B,T", [(2, 1024, 620), (5, 256, 320), (10, 64, 320), (1, 128, 310), (3, 128, 310),
+                                   (4, 128, 310), (6, 64, 305), (7, 64, 305), (8, 64, 305), (9, 64, 305),
                                    (2, 200, 310), (5, 70, 305)])  # ragged: the last block has idle lanes
 def test_free_running_rollout_bit_exact(n, B, T):
     seed = 7 + n
@@ -118,7 +124,31 @@ def _crowded_states(n, B, seed):
     return ora
 
 
-@pytest.mark.parametrize("n,B", [(2, 2048), (5, 512), (10, 128)])
+def _components(e, n):
+    """connected components of an oracle env's contact graph (its arbiters in this step's list):
+    records sharing a dynamic body are connected; segments belong to the static body"""
+    nb = 2 * n + 1
+    parent = list(range(nb))
+
+    def find(x):
+        while parent[x] != x:
+            x = parent[x]
+        return x
+    pairs = [(i, j) for i in range(nb) for j in range(i + 1, nb)]
+    bodies = set()
+    for p in range(npairs(n)):
+        if not e.arb_inlist[p]:
+            continue
+        if p < nb * 12:
+            bodies.add(p // 12)
+        else:
+            i, j = pairs[p - nb * 12]
+            bodies.update((i, j))
+            parent[find(i)] = find(j)
+    return len({find(b) for b in bodies})
+
+
+@pytest.mark.parametrize("n,B", [(2, 2048), (5, 512), (10, 128), (3, 512), (1, 256), (4, 256), (8, 128)])
 def test_teacher_forced_crowded_states(n, B):
     seed = 100 + n
     ora = _crowded_states(n, B, seed)
@@ -132,13 +162,15 @@ def test_teacher_forced_crowded_states(n, B):
     # contact records per env: past the LDS slots (K = 7 / 4 / 2 for N = 2 / 5 / 10) the solve holds
     # the first spill records in registers (0 / 4 / 2 of them) and re-reads the rest from the global
     # spill area in every sweep -- every one of these paths must run
-    lds_slots, reg_spill = {2: 7, 5: 4, 10: 2}[n], {2: 0, 5: 4, 10: 2}[n]
-    most = 0
+    lds_slots, reg_spill = LDS_SLOTS[n], REG_SPILL[n]
+    most = comps = 0
     for t in range(3):
         a = venv.random_actions(900 + t, seed=4321)
         obs, rew, done, _ = venv.step(a)
         o2, r2, d2, _ = ora.step(a.cpu().numpy().astype(np.int32))
         most = max(most, max(int(np.sum(np.asarray(e.arb_inlist))) for e in ora.envs))
+        if n <= 3:  # the per-component split solve (Nb <= 8) must see multi-component envs
+            comps = max(comps, max(_components(e, n) for e in ora.envs))
         assert np.array_equal(done.cpu().numpy(), d2)
         assert np.array_equal(rew.cpu().numpy(), r2), "step %d reward max diff %g" % (
             t, np.abs(rew.cpu().numpy() - r2).max())
@@ -148,10 +180,11 @@ def test_teacher_forced_crowded_states(n, B):
     ex, _, _ = v1_dense_cache(venv.get_state(), n, B)
     assert ex.sum(1).max() > 8, "crowded states must overflow the LDS contact slots"
     assert most > lds_slots + reg_spill, "some env must have records past the register-held spill slots"
+    assert n > 3 or comps >= 2, "some env must have a contact graph of two or more components"
     venv.close()
 
 
-@pytest.mark.parametrize("n,B", [(2, 512), (5, 128), (10, 64)])
+@pytest.mark.parametrize("n,B", [(2, 512), (5, 128), (10, 64), (1, 128), (3, 128), (4, 64), (7, 64)])
 def test_float32_outputs_are_the_cast_of_float64(n, B):
     """The float-output kernel instances (the default of make()) against the double ones."""
     a64, a32 = _venv(n, B, 3, torch.float64), _venv(n, B, 3, torch.float32)
@@ -213,7 +246,7 @@ def test_custom_field_size():
     venv.close()
 
 
-@pytest.mark.parametrize("n,B", [(2, 512), (5, 256)])
+@pytest.mark.parametrize("n,B", [(2, 512), (5, 256), (3, 512), (1, 256), (6, 128)])
 def test_goal_restart_micro_step(n, B):
     """A goal's restart micro-step (space.step(1e-4) from formation) runs the per-lane no-contact
     path: teacher-forced states with the ball about to cross the right goal line (or the left

@@ -40,7 +40,7 @@ def step(e, n, left):
     return obs, r.value, bool(d)
 
 
-@pytest.mark.parametrize("n", [1, 2, 3, 5, 10])
+@pytest.mark.parametrize("n", list(range(1, 11)))
 def test_k1_formation_obs(n):
     """team.py:52-112 formation, futbol_env.py:154-180 normalisation."""
     e = fresh(n)
