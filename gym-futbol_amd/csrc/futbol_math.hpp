@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
+#include "futbol_sincostab.h"
+#include "futbol_powtab.h"
 
 namespace futbol {
 
@@ -150,6 +152,217 @@ __host__ __device__ inline void cr_sincos(double a, double* sn, double* cs)
     else if (q == 1) { *sn = c.h; *cs = -s.h; }
     else if (q == 2) { *sn = -s.h; *cs = -c.h; }
     else { *sn = -c.h; *cs = s.h; }
+}
+
+// ---- glibc 2.35 sin / cos ---------------------------------------------------
+// The reference's screw_vec (envs/futbol_env.py:101-116) rotates a shot by math.sin / math.cos,
+// i.e. glibc's: on x86-64 hosts with FMA + AVX2 (the reference's goldens were produced on one)
+// glibc runs the __sin_fma / __cos_fma build of the IBM Accurate Mathematical Library's
+// sysdeps/ieee754/dbl-64/s_sin.c.  Restated here operation for operation -- do_sin with
+// TAYLOR_SIN below 0.126, do_cos, reduce_sincos, do_sincos, and every multiply-add the compiler
+// fused in that build as an fma -- with glibc's table (futbol_sincostab.h), so the kernel's shot
+// directions are bit-identical to the reference's (oracle/oracle_math.h holds the checker's own
+// restatement, tests/test_glibc_sincos.py pins it against the host libm).  |x| < 105414350 only
+// (screw_vec's angles are below 4.5 in magnitude); beyond, the correctly rounded cr_sincos.
+static constexpr double kSinCosTab[440] = {FUTBOL_SINCOSTAB_ROWS};
+
+namespace glibc_sincos {
+constexpr double BIG = 0x1.8p45, SN3 = -0x1.5555555555515p-3, SN5 = 0x1.11110e829872fp-7;
+constexpr double CS2 = 0x1.0p-1, CS4 = -0x1.5555555555535p-5, CS6 = 0x1.6c16bedd9e239p-10;
+constexpr double S1 = -0x1.5555555555555p-3, S2 = 0x1.1111111110ecep-7, S3 = -0x1.a01a019db08b8p-13,
+                 S4 = 0x1.71de27b9a7ed9p-19, S5 = -0x1.addffc2fcdf59p-26;
+constexpr double HP0 = 0x1.921fb54442d18p0, HP1 = 0x1.1a62633145c07p-54;
+constexpr double HPINV = 0x1.45f306dc9c883p-1, TOINT = 0x1.8p52;
+constexpr double MP1 = 0x1.921fb58p0, MP2 = -0x1.dde973cp-27, PP3 = -0x1.cb3b398p-55, PP4 = -0x1.d747f23e32ed7p-83;
+
+__host__ __device__ inline uint32_t hi_word(double x)
+{
+    uint64_t b;
+    memcpy(&b, &x, 8);
+    return (uint32_t)(b >> 32) & 0x7fffffffu;
+}
+// the table row of |x| (u = |x| + BIG rounds |x| to a multiple of 1/128); rows 0..109
+__host__ __device__ inline const double* row(double u)
+{
+    uint64_t b;
+    memcpy(&b, &u, 8);
+    uint32_t i = (uint32_t)b;
+    i = i < 110u ? i : 109u;  // |x| < 0.8555 keeps i <= 109; the clamp only bounds the address
+    return kSinCosTab + 4 * i;
+}
+__host__ __device__ inline double do_sin(double x, double dx)
+{
+    if (fabs(x) < 0.126) {  // TAYLOR_SIN
+        const double xx = x * x;
+        double p = fma(xx, S5, S4);
+        p = fma(xx, p, S3);
+        p = fma(xx, p, S2);
+        p = fma(xx, p, S1);
+        return x + fma(xx, fma(p, x, -(0.5 * dx)), dx);
+    }
+    const double d = x <= 0 ? -dx : dx;
+    const double ax = fabs(x), u = ax + BIG, xr = ax - (u - BIG);
+    const double* T = row(u);
+    const double xx = xr * xr;
+    const double sv = xr + fma(xr * xx, fma(xx, SN5, SN3), d);
+    const double cv = fma(xr, d, xx * fma(xx, fma(xx, CS6, CS4), CS2));
+    const double cor = fma(sv, T[2], fma(-cv, T[0], fma(sv, T[3], T[1])));
+    return copysign(T[0] + cor, x);
+}
+__host__ __device__ inline double do_cos(double x, double dx)
+{
+    const double d = x < 0 ? -dx : dx;
+    const double ax = fabs(x), u = ax + BIG, xr = (ax - (u - BIG)) + d;
+    const double* T = row(u);
+    const double xx = xr * xr;
+    const double sv = fma(xr * xx, fma(xx, SN5, SN3), xr);
+    const double cv = xx * fma(xx, fma(xx, CS6, CS4), CS2);
+    const double cor = fma(-sv, T[0], fma(-cv, T[2], fma(-sv, T[1], T[3])));
+    return T[2] + cor;
+}
+__host__ __device__ inline int reduce(double x, double& a, double& da)
+{
+    const double t = fma(x, HPINV, TOINT);
+    const double xn = t - TOINT;
+    uint64_t tb;
+    memcpy(&tb, &t, 8);
+    double y = fma(-xn, MP1, x);
+    y = fma(-xn, MP2, y);
+    const double t2 = fma(-xn, PP3, y);
+    const double db = fma(-xn, PP3, y - t2);
+    const double b = fma(-xn, PP4, t2);
+    da = db + fma(-xn, PP4, t2 - b);
+    a = b;
+    return (int)(tb & 3u);
+}
+__host__ __device__ inline double do_sincos(double a, double da, int n)
+{
+    const double r = (n & 1) ? do_cos(a, da) : do_sin(a, da);
+    return (n & 2) ? -r : r;
+}
+}  // namespace glibc_sincos
+
+__host__ __device__ inline double glibc_sin(double x)
+{
+    using namespace glibc_sincos;
+    const uint32_t k = hi_word(x);
+    if (k < 0x3e500000u) return x;
+    if (k < 0x3feb6000u) return do_sin(x, 0.0);
+    if (k < 0x400368fdu) return copysign(do_cos(HP0 - fabs(x), HP1), x);
+    if (k < 0x419921fbu) {
+        double a, da;
+        const int n = reduce(x, a, da);
+        return do_sincos(a, da, n);
+    }
+    double sn, cs;
+    cr_sincos(x, &sn, &cs);
+    return sn;
+}
+__host__ __device__ inline double glibc_cos(double x)
+{
+    using namespace glibc_sincos;
+    const uint32_t k = hi_word(x);
+    if (k < 0x3e400000u) return 1.0;
+    if (k < 0x3feb6000u) return do_cos(x, 0.0);
+    if (k < 0x400368fdu) {
+        const double y = HP0 - fabs(x);
+        const double a = y + HP1;
+        return do_sin(a, (y - a) + HP1);
+    }
+    if (k < 0x419921fbu) {
+        double a, da;
+        const int n = reduce(x, a, da);
+        return do_sincos(a, da, n + 1);
+    }
+    double sn, cs;
+    cr_sincos(x, &sn, &cs);
+    return cs;
+}
+
+// ---- glibc 2.35 pow(x, 2.0) -----------------------------------------------
+// The reference's `x**2` (get_vec, _step_by_observation, _ball_to_team_distance_arr, pymunk's
+// Vec2d.length in limit_velocity) is libm pow(x, 2.0): CPython floats and numpy float64 scalars
+// call it.  glibc's pow (ARM optimized-routines algorithm, the __pow_fma build) computes
+// exp(2 log x) in double-double with 128-entry tables and rounds once at the end; before that
+// rounding it is within 1.11 / 128 + poly error (< 0.009) ulp of x^2, so its result is the
+// correctly rounded x*x unless x^2 lies within that distance of a rounding midpoint (~2% of
+// arguments; the results then differ on ~0.08%).  glibc_pow2: x*x, and the restated glibc
+// computation only where |x^2 - midpoint| < 2^-6 ulp (exact test: lo = fma(x, x, -x*x) is the
+// exact rounding error of x*x).  Main path only: x normal with x^2 in [2^-738, 2^738], x*x
+// elsewhere (never reached by squared coordinate differences).  Tables: futbol_powtab.h.
+static constexpr double kPowLog[128 * 3] = {FUTBOL_POW_LOG_ROWS};
+static constexpr uint64_t kPowExp[256] = {FUTBOL_POW_EXP_ROWS};
+
+__host__ __device__ inline double bits_to_f64(uint64_t u)
+{
+    double d;
+    memcpy(&d, &u, 8);
+    return d;
+}
+__host__ __device__ inline uint64_t f64_to_bits(double d)
+{
+    uint64_t u;
+    memcpy(&u, &d, 8);
+    return u;
+}
+
+// glibc's pow(x, 2.0) computed in full (log_inline, y * log, exp_inline), |x| normal
+__host__ __device__ __attribute__((noinline)) inline double glibc_pow2_full(double x)
+{
+    const uint64_t ix = f64_to_bits(x) & 0x7fffffffffffffffull;  // y even: pow(-x, 2) = pow(x, 2)
+    const uint32_t topx = (uint32_t)(ix >> 52);
+    if (topx < 0x3ff - 369 || topx > 0x3ff + 369) return x * x;
+    const uint64_t tmp = ix - 0x3fe6955500000000ull;
+    const int i = (int)((tmp >> 45) & 127u);
+    const double kd = (double)((int64_t)tmp >> 52);
+    const double z = bits_to_f64(ix - (tmp & 0xfff0000000000000ull));
+    const double invc = kPowLog[3 * i], logc = kPowLog[3 * i + 1], logctail = kPowLog[3 * i + 2];
+    const double r = fma(z, invc, -1.0);
+    const double t1 = fma(kd, 0x1.62e42fefa3800p-1, logc);
+    const double t2 = t1 + r;
+    const double lo1 = fma(kd, 0x1.ef35793c76730p-45, logctail);
+    const double lo2 = (t1 - t2) + r;
+    const double ar = r * -0x1.0p-1;
+    const double ar2 = r * ar, ar3 = r * ar2;
+    const double hi = t2 + ar2;
+    const double lo3 = fma(ar, r, -ar2);
+    const double lo4 = (t2 - hi) + ar2;
+    const double q = fma(ar2, fma(ar2, fma(r, 0x1.0002b8b263fc3p+0, -0x1.2495b9b4845e9p+0),
+                                  fma(r, -0x1.555555529a47ap-1, 0x1.999999959554ep-1)),
+                         fma(r, 0x1.0000000000006p-1, -0x1.5555555555560p-1));
+    const double lo = fma(ar3, q, ((lo1 + lo2) + lo3) + lo4);
+    const double ly = hi + lo, ltail = (hi - ly) + lo;
+    const double ehi = 2.0 * ly;
+    const double elo = fma(2.0, ltail, fma(ly, 2.0, -ehi));
+    const uint32_t abstop = (uint32_t)(f64_to_bits(ehi) >> 52) & 0x7ffu;
+    if (abstop < 0x3c9u) return 1.0 + ehi;
+    if (abstop >= 0x408u) return x * x;
+    double kx = fma(ehi, 0x1.71547652b82fep+7, 0x1.8p52);
+    const uint64_t ki = f64_to_bits(kx);
+    kx = kx - 0x1.8p52;
+    double rr = fma(kx, -0x1.62e42fefa0000p-8, ehi);
+    rr = fma(kx, -0x1.cf79abc9e3b3ap-47, rr);
+    rr = elo + rr;
+    const int idx = 2 * (int)(ki & 127u);
+    const double tail = bits_to_f64(kPowExp[idx]);
+    const double scale = bits_to_f64(kPowExp[idx + 1] + (ki << 45));
+    const double r2 = rr * rr;
+    const double t = fma(r2 * r2, fma(rr, 0x1.1111167a4d017p-7, 0x1.55555cf172b91p-5),
+                         fma(fma(rr, 0x1.555555555543cp-3, 0x1.ffffffffffdbdp-2), r2, tail + rr));
+    return fma(t, scale, scale);
+}
+
+// glibc pow(x, 2.0): x*x unless x^2 is within 2^-6 ulp of a rounding midpoint
+__host__ __device__ __forceinline__ double glibc_pow2(double x)
+{
+    const double h = x * x;
+    const double l = fma(x, x, -h);  // exact: x^2 = h + l, |l| <= ulp(h) / 2
+    // ulp(h) / 2 * (1 - 2^-5) = 2^(e - 53) * (1 - 2^-5), e the exponent of h (h normal, e >= -969:
+    // smaller squares go to the full path, which returns x*x for them)
+    const uint64_t eb = f64_to_bits(h) & 0x7ff0000000000000ull;
+    const double near = bits_to_f64(eb > (54ull << 52) ? eb - (53ull << 52) : 0ull) * (1.0 - 0x1.0p-5);
+    if (__builtin_expect(!(__builtin_fabs(l) < near), 0) && h != 0.0) return glibc_pow2_full(x);
+    return h;
 }
 
 }  // namespace futbol

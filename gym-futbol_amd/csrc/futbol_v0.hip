@@ -39,12 +39,13 @@ struct Env {
     double shot_cs, shot_sn, shot_mag, shot_acc;
 };
 
-// get_vec (:62-65): vector from o to t and its magnitude
+// get_vec (:62-65): vector from o to t and its magnitude; `vec[0]**2` is numpy's float64 power,
+// i.e. libm pow(x, 2.0) (glibc_pow2, futbol_math.hpp)
 __device__ __forceinline__ double get_vec(double tx, double ty, double ox, double oy, double& vx, double& vy)
 {
     vx = tx - ox;
     vy = ty - oy;
-    return sqrt(vx * vx + vy * vy);
+    return sqrt(glibc_pow2(vx) + glibc_pow2(vy));
 }
 
 __device__ __forceinline__ double intercept_chance(double d) /* :122-129, d1 = 1, d2 = 2 */
@@ -216,7 +217,7 @@ __device__ __forceinline__ int get_action_type(const Ctx& c, const Env& e, bool 
 __device__ __forceinline__ void step_by_observation(double* o)
 {
     const double tx = o[2], ty = o[3];
-    const double mag = sqrt(tx * tx + ty * ty);
+    const double mag = sqrt(glibc_pow2(tx) + glibc_pow2(ty));
     if (mag != 0) {
         o[0] = o[0] + o[4] * (tx * STEP_SIZE / mag);
         o[1] = o[1] + o[4] * (ty * STEP_SIZE / mag);
@@ -232,8 +233,8 @@ __device__ __forceinline__ void resolve_shot(Env& e, const Stream& rs)
     if (!e.shot) return;
     const double nd = Stream::normal_of(rs.block(e.shot_pos), 0.0, e.shot_acc);
     const double ang = (nd / 180) * 3.141592653589793;
-    double ss, sc;
-    cr_sincos(ang, &ss, &sc);
+    // math.sin / math.cos of the reference: glibc's (futbol_math.hpp glibc_sin / glibc_cos)
+    const double ss = glibc_sin(ang), sc = glibc_cos(ang);
     const double cs = e.shot_cs, sn = e.shot_sn;
     const double tc = (cs * sc) - (sn * ss), ts = (sn * sc) + (cs * ss);
     e.r[BALL][2] = tc * e.shot_mag;

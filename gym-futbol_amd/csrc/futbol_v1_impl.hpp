@@ -33,6 +33,7 @@
 #include <type_traits>
 #include "futbol_kernels.hpp"
 #include "futbol_v1_params.hpp"
+#include "futbol_math.hpp"
 #include "futbol_rng.hpp"
 #include "futbol_state.hpp"
 #include "futbol_util.hpp"
@@ -871,7 +872,8 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
         constexpr int k = K;
         e.vx[k] = e.vx[k] * damping + 0.0 * dt;
         e.vy[k] = e.vy[k] * damping + 0.0 * dt;
-        const double s2 = e.vx[k] * e.vx[k] + e.vy[k] * e.vy[k];
+        // the callback's l = Vec2d.length = sqrt(x**2 + y**2): Python pow squares (glibc_pow2)
+        const double s2 = glibc_pow2(e.vx[k]) + glibc_pow2(e.vy[k]);
         const double thr = k == S::BALL ? P.clamp2_ball : P.clamp2_player;
         if (s2 > thr) {
             constexpr double vmax = k == S::BALL ? kBallVmax : kPlayerVmax;
@@ -908,7 +910,10 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
         uint64_t cm = whole;
         uint32_t cbase = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
         int total = __popcll(act);
-        constexpr int FW = kSlotBits<N>;
+        // slot-mask field width: the component fields, or one 8-bit field holding all K <= 8 LDS slots
+        // of a whole-env item (a 4-bit field would drop slot 4 of the N = 4 instance's K = 5)
+        constexpr int FW = kSolveComponents<N> ? kSlotBits<N> : 8;
+        static_assert(kSolveComponents<N> || KL <= 8, "whole-env items hold at most 8 LDS slots");
         constexpr int NFLD = kSolveComponents<N> ? (FW == 8 ? 8 : S::Nb) : 1;  // slot-mask fields
         if constexpr (kSolveComponents<N>) {
             const uint64_t cc = n > KL ? whole : cslots;
@@ -1567,7 +1572,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
     sfor<N>([&](auto I) {
         constexpr int i = I;
         const double dx = e.px[i] - e.px[BL], dy = e.py[i] - e.py[BL];
-        d0[i] = sqrt(dx * dx + dy * dy);
+        d0[i] = sqrt(glibc_pow2(dx) + glibc_pow2(dy));  // math.sqrt((px-bx)**2 + (py-by)**2)
     });
     const double bix = e.px[BL], biy = e.py[BL];
 
@@ -1614,7 +1619,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
         const double ox = press ? e.px[k] : e.px[BL], oy = press ? e.py[k] : e.py[BL];
         const double qx = press ? e.px[BL] : (shoot ? gx : tx), qy = press ? e.py[BL] : (shoot ? gy : ty);
         const double dx = qx - ox, dy = qy - oy;
-        const double mag = sqrt(dx * dx + dy * dy);
+        const double mag = sqrt(glibc_pow2(dx) + glibc_pow2(dy));  // get_vec (:56-59): Python `**2`
         const double S = press ? 40.0 : (shoot ? 120.0 : 100.0);
         const double fdx = S * dx / mag, fdy = S * dy / mag;
         // player velocity: move impulse (f * arrow) / m, or the press impulse
@@ -1714,7 +1719,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
                 sfor<N>([&](auto I) {
                     constexpr int i = I;
                     const double dx = e.px[i] - e.px[BL], dy = e.py[i] - e.py[BL];
-                    const double diff = d0[i] - sqrt(dx * dx + dy * dy);
+                    const double diff = d0[i] - sqrt(glibc_pow2(dx) + glibc_pow2(dy));
                     if constexpr (N == 5) {
                         if constexpr (i == 3) mx = diff;
                         if constexpr (i == 4) mx = diff > mx ? diff : mx;
@@ -1726,7 +1731,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
                 const double gx = W, gy = H / 2;
                 const double ax_ = e.px[BL] - gx, ay_ = e.py[BL] - gy;
                 const double ix_ = bix - gx, iy_ = biy - gy;
-                r = r + (sqrt(ix_ * ix_ + iy_ * iy_) - sqrt(ax_ * ax_ + ay_ * ay_)) * 10;
+                r = r + (sqrt(glibc_pow2(ix_) + glibc_pow2(iy_)) - sqrt(glibc_pow2(ax_) + glibc_pow2(ay_))) * 10;
             }
             // ball_contact_goal (:291-296), tested by space_step on the final positions; a goal
             // restarts from formation, the episode goes on

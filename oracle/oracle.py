@@ -65,6 +65,7 @@ def lib(portable=False):
     L.orc_v1_vec_step.argtypes = [C.c_void_p, C.c_int, ip, dp, dp, up, C.c_void_p, C.c_int]
     L.orc_v1_run.argtypes = [C.c_void_p, C.c_int, C.c_uint64, C.POINTER(C.c_double)]
     L.orc_v1_run.restype = C.c_int
+    L.orc_libm_check.argtypes = [C.c_int64, C.c_double, C.c_double, C.c_uint64] + [C.POINTER(C.c_int64)] * 3
     L.orc_v0_init.argtypes = [C.c_void_p] + [C.c_double] * 6 + [C.c_int] * 3 + [C.c_uint64, C.c_uint32]
     L.orc_v0_reset.argtypes = [C.c_void_p, C.c_void_p]
     L.orc_v0_step.argtypes = [C.c_void_p, C.c_int32, C.c_int32, dp, C.POINTER(C.c_double)]

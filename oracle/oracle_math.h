@@ -156,10 +156,211 @@ static inline void orc_cr_sincos(double a, double *sn, double *cs)
     else { *sn = -c.h; *cs = s.h; }
 }
 
+/* ---- glibc 2.35 sin / cos, restated (the reference's math.sin / math.cos in screw_vec,
+ * envs/futbol_env.py:109-110, run glibc's; CPython calls libm directly).  The IBM Accurate
+ * Mathematical Library algorithm of sysdeps/ieee754/dbl-64/s_sin.c (do_sin, do_cos, TAYLOR_SIN,
+ * reduce_sincos, do_sincos) as compiled into the variant glibc selects on x86-64 hosts with FMA and
+ * AVX2 (__sin_fma / __cos_fma, the one this image's CPUs run): every a*b+c the compiler fused is
+ * an fma() here, in the same association.  Table: glibc's __sincostab (futbol_sincostab.h,
+ * scripts/gen_sincostab.py).  Valid for |x| < 105414350 (the __branred range is never reached by
+ * screw_vec's angles, |x| < 4.5); pinned against the host libm by tests/test_glibc_sincos.py. */
+#include "../gym-futbol_amd/csrc/futbol_sincostab.h"
+static const double ORC_SINCOSTAB[440] = { FUTBOL_SINCOSTAB_ROWS };
+#define ORC_G_BIG 0x1.8p45
+#define ORC_G_SN3 (-0x1.5555555555515p-3)
+#define ORC_G_SN5 0x1.11110e829872fp-7
+#define ORC_G_CS2 0x1.0p-1
+#define ORC_G_CS4 (-0x1.5555555555535p-5)
+#define ORC_G_CS6 0x1.6c16bedd9e239p-10
+#define ORC_G_S1 (-0x1.5555555555555p-3)
+#define ORC_G_S2 0x1.1111111110ecep-7
+#define ORC_G_S3 (-0x1.a01a019db08b8p-13)
+#define ORC_G_S4 0x1.71de27b9a7ed9p-19
+#define ORC_G_S5 (-0x1.addffc2fcdf59p-26)
+#define ORC_G_HP0 0x1.921fb54442d18p0
+#define ORC_G_HP1 0x1.1a62633145c07p-54
+#define ORC_G_HPINV 0x1.45f306dc9c883p-1
+#define ORC_G_TOINT 0x1.8p52
+#define ORC_G_MP1 0x1.921fb58p0
+#define ORC_G_MP2 (-0x1.dde973cp-27)
+#define ORC_G_PP3 (-0x1.cb3b398p-55)
+#define ORC_G_PP4 (-0x1.d747f23e32ed7p-83)
+
+static inline int orc_g_index(double u)
+{
+    uint64_t b;
+    memcpy(&b, &u, 8);
+    return (int)((uint32_t)b << 2);
+}
+static inline uint32_t orc_g_hi(double x)
+{
+    uint64_t b;
+    memcpy(&b, &x, 8);
+    return (uint32_t)(b >> 32) & 0x7fffffffu;
+}
+/* do_sin (x, dx), TAYLOR_SIN below |x| = 0.126 */
+static inline double orc_g_do_sin(double x, double dx)
+{
+    if (fabs(x) < 0.126) {
+        const double xx = x * x;
+        double p = fma(xx, ORC_G_S5, ORC_G_S4);
+        p = fma(xx, p, ORC_G_S3);
+        p = fma(xx, p, ORC_G_S2);
+        p = fma(xx, p, ORC_G_S1);
+        return x + fma(xx, fma(p, x, -(0.5 * dx)), dx);
+    }
+    if (x <= 0) dx = -dx;
+    const double ax = fabs(x);
+    const double u = ax + ORC_G_BIG;
+    const double xr = ax - (u - ORC_G_BIG);
+    const int k = orc_g_index(u);
+    const double *T = ORC_SINCOSTAB + k;
+    const double xx = xr * xr;
+    const double s = xr + fma(xr * xx, fma(xx, ORC_G_SN5, ORC_G_SN3), dx);
+    const double c = fma(xr, dx, xx * fma(xx, fma(xx, ORC_G_CS6, ORC_G_CS4), ORC_G_CS2));
+    const double cor = fma(s, T[2], fma(-c, T[0], fma(s, T[3], T[1])));
+    return copysign(T[0] + cor, x);
+}
+/* do_cos (x, dx) */
+static inline double orc_g_do_cos(double x, double dx)
+{
+    if (x < 0) dx = -dx;
+    const double ax = fabs(x);
+    const double u = ax + ORC_G_BIG;
+    const double xr = (ax - (u - ORC_G_BIG)) + dx;
+    const int k = orc_g_index(u);
+    const double *T = ORC_SINCOSTAB + k;
+    const double xx = xr * xr;
+    const double s = fma(xr * xx, fma(xx, ORC_G_SN5, ORC_G_SN3), xr);
+    const double c = xx * fma(xx, fma(xx, ORC_G_CS6, ORC_G_CS4), ORC_G_CS2);
+    const double cor = fma(-s, T[0], fma(-c, T[2], fma(-s, T[1], T[3])));
+    return T[2] + cor;
+}
+/* reduce_sincos: x = n pi/2 + a + da */
+static inline int orc_g_reduce(double x, double *a, double *da)
+{
+    const double t = fma(x, ORC_G_HPINV, ORC_G_TOINT);
+    const double xn = t - ORC_G_TOINT;
+    uint64_t tb;
+    memcpy(&tb, &t, 8);
+    double y = fma(-xn, ORC_G_MP1, x);
+    y = fma(-xn, ORC_G_MP2, y);
+    const double t2 = fma(-xn, ORC_G_PP3, y);
+    const double db = fma(-xn, ORC_G_PP3, y - t2);
+    const double b = fma(-xn, ORC_G_PP4, t2);
+    *da = db + fma(-xn, ORC_G_PP4, t2 - b);
+    *a = b;
+    return (int)(tb & 3);
+}
+static inline double orc_g_do_sincos(double a, double da, int n)
+{
+    const double r = (n & 1) ? orc_g_do_cos(a, da) : orc_g_do_sin(a, da);
+    return (n & 2) ? -r : r;
+}
+static inline double orc_glibc_sin(double x)
+{
+    const uint32_t k = orc_g_hi(x);
+    if (k < 0x3e500000u) return x;
+    if (k < 0x3feb6000u) return orc_g_do_sin(x, 0.0);
+    if (k < 0x400368fdu) return copysign(orc_g_do_cos(ORC_G_HP0 - fabs(x), ORC_G_HP1), x);
+    if (k < 0x419921fbu) {
+        double a, da;
+        const int n = orc_g_reduce(x, &a, &da);
+        return orc_g_do_sincos(a, da, n);
+    }
+    double s, c;  /* outside screw_vec's range: correctly rounded instead of __branred */
+    orc_cr_sincos(x, &s, &c);
+    return s;
+}
+static inline double orc_glibc_cos(double x)
+{
+    const uint32_t k = orc_g_hi(x);
+    if (k < 0x3e400000u) return 1.0;
+    if (k < 0x3feb6000u) return orc_g_do_cos(x, 0.0);
+    if (k < 0x400368fdu) {
+        const double y = ORC_G_HP0 - fabs(x);
+        const double a = y + ORC_G_HP1;
+        const double da = (y - a) + ORC_G_HP1;
+        return orc_g_do_sin(a, da);
+    }
+    if (k < 0x419921fbu) {
+        double a, da;
+        const int n = orc_g_reduce(x, &a, &da);
+        return orc_g_do_sincos(a, da, n + 1);
+    }
+    double s, c;
+    orc_cr_sincos(x, &s, &c);
+    return c;
+}
+
+/* ---- glibc 2.35 pow(x, 2.0), restated: the reference's `x**2` (CPython float and numpy float64
+ * powers call libm pow).  glibc's pow is exp(y log x) in double-double (ARM optimized-routines
+ * algorithm, sysdeps/ieee754/dbl-64/e_pow.c; the __pow_fma build with its fused multiply-adds as
+ * fma() here), NOT x*x: the two differ on ~0.08% of arguments.  Main path only (x normal and
+ * x^2 within [2^-738, 2^738]; elsewhere x*x -- squares of the envs' coordinates never leave it).
+ * Tables: futbol_powtab.h (scripts/gen_powtab.py). */
+#include "../gym-futbol_amd/csrc/futbol_powtab.h"
+static const double ORC_POW_LOG[128 * 3] = { FUTBOL_POW_LOG_ROWS };
+static const uint64_t ORC_POW_EXP[256] = { FUTBOL_POW_EXP_ROWS };
+static inline double orc_asd(uint64_t u) { double d; memcpy(&d, &u, 8); return d; }
+static inline uint64_t orc_asu(double d) { uint64_t u; memcpy(&u, &d, 8); return u; }
+static inline double orc_glibc_pow2(double x)
+{
+    const double Y = 2.0;
+    uint64_t ix = orc_asu(x) & 0x7fffffffffffffffULL;   /* y even: pow(-x, 2) = pow(x, 2) */
+    const uint32_t topx = (uint32_t)(ix >> 52);
+    if (topx == 0 || topx >= 0x7ff || topx < 0x3ff - 369 || topx > 0x3ff + 369) return x * x;
+    /* log_inline */
+    const uint64_t tmp = ix - 0x3fe6955500000000ULL;
+    const int i = (int)((tmp >> 45) & 127);
+    const int64_t k = (int64_t)tmp >> 52;
+    const double z = orc_asd(ix - (tmp & 0xfff0000000000000ULL));
+    const double kd = (double)k;
+    const double invc = ORC_POW_LOG[3 * i], logc = ORC_POW_LOG[3 * i + 1], logctail = ORC_POW_LOG[3 * i + 2];
+    const double r = fma(z, invc, -1.0);
+    const double t1 = fma(kd, 0x1.62e42fefa3800p-1, logc);
+    const double t2 = t1 + r;
+    const double lo1 = fma(kd, 0x1.ef35793c76730p-45, logctail);
+    const double lo2 = (t1 - t2) + r;
+    const double ar = r * -0x1.0p-1;
+    const double ar2 = r * ar, ar3 = r * ar2;
+    const double hi = t2 + ar2;
+    const double lo3 = fma(ar, r, -ar2);
+    const double lo4 = (t2 - hi) + ar2;
+    const double q = fma(ar2, fma(ar2, fma(r, 0x1.0002b8b263fc3p+0, -0x1.2495b9b4845e9p+0),
+                                  fma(r, -0x1.555555529a47ap-1, 0x1.999999959554ep-1)),
+                         fma(r, 0x1.0000000000006p-1, -0x1.5555555555560p-1));
+    const double lo = fma(ar3, q, ((lo1 + lo2) + lo3) + lo4);
+    const double ly = hi + lo;
+    const double ltail = (hi - ly) + lo;
+    /* y * log x */
+    const double ehi = Y * ly;
+    const double elo = fma(Y, ltail, fma(ly, Y, -ehi));
+    /* exp_inline (sign_bias 0) */
+    const uint32_t abstop = (uint32_t)(orc_asu(ehi) >> 52) & 0x7ff;
+    if (abstop < 0x3c9) return 1.0 + ehi;                      /* |ehi| < 2^-54 */
+    if (abstop >= 0x408) return x * x;                         /* outside the squares' range */
+    double kx = fma(ehi, 0x1.71547652b82fep+7, 0x1.8p52);
+    const uint64_t ki = orc_asu(kx);
+    kx = kx - 0x1.8p52;
+    double rr = fma(kx, -0x1.62e42fefa0000p-8, ehi);
+    rr = fma(kx, -0x1.cf79abc9e3b3ap-47, rr);
+    rr = elo + rr;
+    const int idx = 2 * (int)(ki & 127);
+    const uint64_t top = ki << 45;
+    const double tail = orc_asd(ORC_POW_EXP[idx]);
+    const double scale = orc_asd(ORC_POW_EXP[idx + 1] + top);
+    const double r2 = rr * rr;
+    const double t = fma(r2 * r2, fma(rr, 0x1.1111167a4d017p-7, 0x1.55555cf172b91p-5),
+                         fma(fma(rr, 0x1.555555555543cp-3, 0x1.ffffffffffdbdp-2), r2, tail + rr));
+    return fma(t, scale, scale);
+}
+
 #ifdef ORACLE_PORTABLE
-#define ORC_SQ(x) ((x) * (x))
-static inline double ORC_SIN(double x) { double s, c; orc_cr_sincos(x, &s, &c); return s; }
-static inline double ORC_COS(double x) { double s, c; orc_cr_sincos(x, &s, &c); return c; }
+/* the kernels' arithmetic: the glibc pow(x, 2.0) and sin / cos restatements above */
+#define ORC_SQ(x) orc_glibc_pow2(x)
+#define ORC_SIN(x) orc_glibc_sin(x)
+#define ORC_COS(x) orc_glibc_cos(x)
 #else
 #define ORC_SQ(x) pow((x), 2.0)
 #define ORC_SIN(x) sin(x)

@@ -1,9 +1,9 @@
-# smoke + GPU parity tests + bench (+ optional rocprofv3 passes), via gpurun from the repo root
+# smoke, the -m gpu suite and the C2 bench line (run via gpurun from the repo root)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out
-rocm-smi --showproductname > gpurun_out/smi.txt 2>&1 || true
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1 && \
-timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1 && \
-if [ -n "$PROFILE" ]; then bash scripts/gpu_profile.sh > gpurun_out/profile.log 2>&1; fi
+O=gpurun_out/${OUT_DIR:-check}
+mkdir -p $O
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \
+timeout -k 10 1200 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ${PYTEST_ARGS:-} > $O/pytest_gpu.log 2>&1 && \
+timeout -k 10 300 python bench.py > $O/bench.log 2>&1
+echo rc=$?

@@ -1,6 +1,7 @@
 """Generate v0 golden vectors by running THE REFERENCE itself (this container only).
 
     python tests/golden/gen_v0_golden.py          # writes tests/golden/v0_*.npz
+    python tests/golden/gen_v0_golden.py --scale  # only the 1 024-env fingerprint sets (v0_scale_*.npz)
 
 The reference (`/root/reference/gym_futbol/envs/futbol_env.py`, `easy_agent.py`)
 is imported behind a throw-away `gym` stand-in written to a temp directory
@@ -104,7 +105,7 @@ def install_stub():
     return d
 
 
-def run(random_opp, n_envs, n_steps, seed, act_seed):
+def run(random_opp, n_envs, n_steps, seed, act_seed, env0=0):
     import gym_futbol.envs.futbol_env as fe  # noqa: the reference
 
     drv = TapeDriver(seed)
@@ -122,28 +123,63 @@ def run(random_opp, n_envs, n_steps, seed, act_seed):
     done = np.zeros((n_envs, n_steps), np.uint8)
     ndraw = np.zeros((n_envs, n_steps), np.int32)
     obs0 = np.zeros((n_envs, 6, 5), np.float64)
-    for e in range(n_envs):
+    for ei in range(n_envs):
+        e = env0 + ei
         event = 0
         drv.begin(e, event); event += 1
         env = fe.FutbolEnv(random_opp=random_opp)
         drv.begin(e, event); event += 1
-        obs0[e] = env.reset()
+        obs0[ei] = env.reset()
         for t in range(n_steps):
             a = synthetic_action(act_seed, e, t, 0, 16)
-            acts[e, t] = a
+            acts[ei, t] = a
             drv.begin(e, event); event += 1
             d0 = drv.draws
             o, r, d, _ = env.step(a)
-            ndraw[e, t] = drv.draws - d0
-            obs[e, t] = o
-            rew[e, t] = r
-            done[e, t] = d
+            ndraw[ei, t] = drv.draws - d0
+            obs[ei, t] = o
+            rew[ei, t] = r
+            done[ei, t] = d
             if d:
-                term[e, t] = o
+                term[ei, t] = o
                 drv.begin(e, event); event += 1
-                obs[e, t] = env.reset()
+                obs[ei, t] = env.reset()
     return dict(actions=acts, obs=obs, terminal_obs=term, reward=rew, done=done, draws=ndraw, obs0=obs0,
                 seed=np.uint64(seed), act_seed=np.uint64(act_seed), random_opp=np.int32(random_opp))
+
+
+def _run_chunk(args):
+    """worker: envs [e0, e1) of one scale case (env ids are global: the tape is keyed by them)"""
+    ro, e0, e1, T, seed, aseed = args
+    stub = install_stub()
+    sys.path[:0] = [stub, REFERENCE]
+    import warnings
+    warnings.simplefilter("ignore", DeprecationWarning)
+    from golden_digest import obs_digest
+    out = run(ro, e1 - e0, T, seed, aseed, env0=e0)
+    return dict(reward=out["reward"], done=out["done"], draws=out["draws"].astype(np.uint8),
+                obs_digest=obs_digest(out["obs"].reshape(e1 - e0, T, 30)),
+                term_digest=np.where(out["done"] != 0, obs_digest(out["terminal_obs"].reshape(e1 - e0, T, 30)), 0)
+                .astype(np.uint32),
+                owner=np.argmax(out["obs"][:, :, 5, :], axis=-1).astype(np.uint8),
+                obs0=out["obs0"])
+
+
+def run_scale(ro, E, T, seed, aseed, workers):
+    """E envs x T steps of the reference, as compact fingerprints (tests/golden_digest.py): exact
+    rewards, dones, RNG draws per step, the ball owner and 32-bit digests of every observation."""
+    from multiprocessing import Pool
+    step = (E + workers - 1) // workers
+    chunks = [(ro, e0, min(E, e0 + step), T, seed, aseed) for e0 in range(0, E, step)]
+    with Pool(len(chunks)) as pool:
+        parts = pool.map(_run_chunk, chunks)
+    out = {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
+    out.update(seed=np.uint64(seed), act_seed=np.uint64(aseed), random_opp=np.int32(ro))
+    return out
+
+
+SCALE_CASES = [("v0_scale_hardcoded_opp.npz", False, 1024, 900, 20240601, 1234),
+               ("v0_scale_random_opp.npz", True, 1024, 900, 777, 99)]
 
 
 def main():
@@ -154,13 +190,21 @@ def main():
     sys.path[:0] = [stub, REFERENCE]
     import warnings
     warnings.simplefilter("ignore", DeprecationWarning)  # randint(32.0, 36.0) on py3.10
-    cases = [("v0_hardcoded_opp.npz", False, 6, 900, 20240601, 1234),
-             ("v0_random_opp.npz", True, 4, 500, 777, 99)]
-    for fname, ro, E, T, seed, aseed in cases:
-        out = run(ro, E, T, seed, aseed)
-        np.savez_compressed(os.path.join(HERE, fname), **out)
-        print(fname, "episodes done:", int(out["done"].sum()), "goals:",
-              int((np.abs(out["reward"]) >= 900).sum()), "draws/step mean:", float(out["draws"].mean()))
+    if "--scale" not in sys.argv:
+        cases = [("v0_hardcoded_opp.npz", False, 6, 900, 20240601, 1234),
+                 ("v0_random_opp.npz", True, 4, 500, 777, 99)]
+        for fname, ro, E, T, seed, aseed in cases:
+            out = run(ro, E, T, seed, aseed)
+            np.savez_compressed(os.path.join(HERE, fname), **out)
+            print(fname, "episodes done:", int(out["done"].sum()), "goals:",
+                  int((np.abs(out["reward"]) >= 900).sum()), "draws/step mean:", float(out["draws"].mean()))
+    if "--small" not in sys.argv:
+        workers = min(8, os.cpu_count() or 1)
+        for fname, ro, E, T, seed, aseed in SCALE_CASES:
+            out = run_scale(ro, E, T, seed, aseed, workers)
+            np.savez_compressed(os.path.join(HERE, fname), **out)
+            print(fname, "envs", E, "steps", T, "episodes done:", int(out["done"].sum()), "goals:",
+                  int((np.abs(out["reward"]) >= 900).sum()))
 
 
 if __name__ == "__main__":

@@ -116,3 +116,25 @@ def synthetic_action(seed, env_id, step, j, n):
     per Philox block, action j = (w * n) >> 32 with w = word j % 4 of block j // 4."""
     x = philox4x32_10((j // 4, step & MASK, env_id & MASK, 1), (seed & MASK, (seed >> 32) & MASK))
     return (x[j % 4] * n) >> 32
+
+
+def synthetic_actions_vec(seed, env_ids, step, j, n):
+    """synthetic_action for an array of env ids at once (numpy, same Philox4x32-10 arithmetic)."""
+    import numpy as np
+    env_ids = np.asarray(env_ids, dtype=np.uint64)
+    m = np.uint64(MASK)
+    c0 = np.full(env_ids.shape, j // 4, np.uint64)
+    c1 = np.full(env_ids.shape, step & MASK, np.uint64)
+    c2 = env_ids & m
+    c3 = np.full(env_ids.shape, 1, np.uint64)
+    k0, k1 = seed & MASK, (seed >> 32) & MASK
+    for r in range(10):
+        if r:
+            k0 = (k0 + W0) & MASK
+            k1 = (k1 + W1) & MASK
+        p0 = np.uint64(M0) * c0
+        p1 = np.uint64(M1) * c2
+        c0, c1, c2, c3 = (((p1 >> np.uint64(32)) ^ c1 ^ np.uint64(k0)) & m, p1 & m,
+                          ((p0 >> np.uint64(32)) ^ c3 ^ np.uint64(k1)) & m, p0 & m)
+    w = (c0, c1, c2, c3)[j % 4]
+    return ((w * np.uint64(n)) >> np.uint64(32)).astype(np.int64)
