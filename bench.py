@@ -157,6 +157,27 @@ def cpu_baseline(kind, n, budget_s=10.0, B=65536):
     return out
 
 
+def rollout_companion(args):
+    """The same workload stepped by open-loop rollout launches (futbol_rollout, 100 steps per launch:
+    the synthetic actions do not depend on the observations, so a launch can run many steps and its
+    blocks never wait for each other between steps), measured by a child bench.py run.  Reported
+    beside `value`, which stays the one-launch-per-step (lockstep, DummyVecEnv) rate."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--steps", str(args.steps), "--warmup", str(args.warmup),
+           "--envs", str(args.envs), "--players", str(args.players), "--kind", args.kind, "--rollout", "100",
+           "--no-cpu-baseline", "--no-rollout-line", "--stagger", str(args.stagger)]
+    try:
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        ln = [x for x in out.stdout.splitlines() if x.startswith("{")][-1]
+        d = json.loads(ln)
+    except Exception as e:  # noqa: BLE001 - report, never fail the main line
+        return {"error": repr(e)[:300]}
+    r = d["roofline"]
+    return {"value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"], "steps_per_launch": 100,
+            "kernel_ms_per_step": r["kernel_ms"], "achieved": r["achieved"], "frac": r["frac"],
+            "launch": d["config"]["launch"], "command": " ".join(["bench.py"] + cmd[2:])}
+
+
 def copy_ceiling(dev, mib=1024, reps=10):
     """Measured HBM stream-copy ceiling (SURVEY 8(d) Roofline): futbol_stream_copy of a `mib` MiB
     buffer (16 B per lane), HIP events on the launch stream; GB/s = 2 x bytes / time."""
@@ -280,6 +301,11 @@ def main():
     ap.add_argument("--stagger", type=int, default=0,
                     help="1: spread the envs' episode starts over an episode (slower: every wave then mixes "
                          "contact-heavy and formation phases); 0: all envs in lockstep as DummyVecEnv runs them")
+    ap.add_argument("--rollout", type=int, default=0,
+                    help="N > 0: step with open-loop rollout launches of up to N steps each (futbol_rollout: the "
+                         "synthetic actions do not depend on the observations), instead of one launch per step")
+    ap.add_argument("--no-rollout-line", action="store_true",
+                    help="skip the open_loop_rollout companion measurement (a child bench.py --rollout 100 run)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=600,
                     help="steps timed per-kernel with HIP events (a multiple of the episode length)")
@@ -349,13 +375,22 @@ def main():
     acts = torch.empty((args.profile_steps,) + tuple(act.shape), dtype=torch.uint8, device=dev)
     for t in range(args.profile_steps):
         venv.random_actions(10**6 + t, seed=1234, out=acts[t])
+    RL = max(0, int(args.rollout))
+    rbuf = None
+    if RL:  # the rollout launches' output buffers [RL, B, ...] (reused by every launch)
+        rbuf = venv.rollout(acts[:min(RL, args.profile_steps)].contiguous())
     kg = torch.cuda.CUDAGraph()
     s = torch.cuda.Stream(dev)
     s.wait_stream(stream)
     with torch.cuda.stream(s):
         with torch.cuda.graph(kg, stream=s):
-            for t in range(args.profile_steps):
-                venv.step_raw(acts[t])
+            if RL:
+                for t0_ in range(0, args.profile_steps, RL):
+                    n_ = min(RL, args.profile_steps - t0_)
+                    venv.rollout(acts[t0_:t0_ + n_], out=tuple(b[:n_] for b in rbuf))
+            else:
+                for t in range(args.profile_steps):
+                    venv.step_raw(acts[t])
     stream.wait_stream(s)
     torch.cuda.synchronize(dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -366,10 +401,18 @@ def main():
     kernel_ms = e0.elapsed_time(e1) / args.profile_steps
     del kg, acts
     venv.kernel_timing(True)
-    for _ in range(args.profile_steps):
-        one_step()
-    tot_ms, cnt = venv.kernel_timing(False)
-    kernel_ms_dispatch = tot_ms / max(cnt, 1)
+    if RL:
+        a_ = venv.random_actions_steps(min(RL, args.profile_steps), ALL, seed=1234)
+        for _ in range(max(1, args.profile_steps // RL)):
+            venv.rollout(a_, out=tuple(b[:a_.shape[0]] for b in rbuf))
+        tot_ms, cnt = venv.kernel_timing(False)
+        kernel_ms_dispatch = tot_ms / max(cnt * a_.shape[0], 1)
+        del a_
+    else:
+        for _ in range(args.profile_steps):
+            one_step()
+        tot_ms, cnt = venv.kernel_timing(False)
+        kernel_ms_dispatch = tot_ms / max(cnt, 1)
 
     if args.stamps:
         return stamps_report(venv, one_step, args)
@@ -405,13 +448,22 @@ def main():
 
     chunks = [(t0_, min(Gs, args.steps - t0_)) for t0_ in range(0, args.steps, Gs)]
 
+    rbufs = {}
+
     def capture(ge, s, abuf, t0_, nsteps):
         g_ = torch.cuda.CUDAGraph()
         s.wait_stream(stream)
         with torch.cuda.stream(s):
+            if RL and id(ge) not in rbufs:
+                rbufs[id(ge)] = ge.rollout(abuf[t0_:t0_ + min(RL, nsteps)].contiguous())
             with torch.cuda.graph(g_, stream=s):
-                for t in range(nsteps):
-                    ge.step_raw(abuf[t0_ + t])
+                if RL:  # one open-loop rollout launch per RL steps of the chunk
+                    for r0 in range(0, nsteps, RL):
+                        n_ = min(RL, nsteps - r0)
+                        ge.rollout(abuf[t0_ + r0:t0_ + r0 + n_], out=tuple(b[:n_] for b in rbufs[id(ge)]))
+                else:
+                    for t in range(nsteps):
+                        ge.step_raw(abuf[t0_ + t])
         stream.wait_stream(s)
         return g_
 
@@ -537,6 +589,8 @@ def main():
                                % args.steps) if graphs is not None else
                               "synthetic Philox left-team actions drawn by a fill launch before every step (timed)",
                    "action_fill_ms_per_step": fill_ms,
+                   "launch": ("open-loop rollout launches of up to %d steps (futbol_rollout; every step writes its "
+                              "obs / reward / done slice)" % RL) if RL else "one futbol_step launch per step",
                    "episode_phases": "staggered" if args.stagger else "lockstep (DummyVecEnv)",
                    "timed_from_episode_step": None if args.stagger else
                    (args.warmup + 2 * args.profile_steps + (args.steps if graphs is not None else 0) + align)
@@ -550,8 +604,10 @@ def main():
                      "copy_ceiling": ceil,
                      "kernel": "v1_step_kernel<%d,float>" % n if args.kind == "v1" else "v0_step_kernel<float>",
                      "kernel_ms": kernel_ms, "kernel_ms_dispatch_events": kernel_ms_dispatch,
-                     "kernel_timing": "HIP events around a hipGraph of %d back-to-back step launches"
-                                      % args.profile_steps,
+                     "kernel_timing": ("HIP events around a hipGraph of %d back-to-back step launches"
+                                       % args.profile_steps) if not RL else
+                                      ("HIP events around a hipGraph of %d steps as rollout launches of %d steps; "
+                                       "per step" % (args.profile_steps, RL)),
                      "algo_bytes_per_launch": per_env * B,
                      "algo_bytes_per_env_step": per_env, "traffic_source": traffic_src},
         "episodes": {"finished": float(stats[1]),
@@ -559,6 +615,8 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.kind, n)
+    if rank == 0 and world == 1 and not RL and not args.no_rollout_line and args.graph:
+        line["open_loop_rollout"] = rollout_companion(args)
     if rank == 0:
         print(json.dumps(line), flush=True)
     for ge in groups:

@@ -34,6 +34,9 @@ CFLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-ffp-contract=off", "-
 PHI = os.environ.get("FUTBOL_PHI_FOLD", "20")
 PHI_SOURCES = {"futbol_v1_n1_e64.hip": PHI, "futbol_v1_n2_e64.hip": PHI, "futbol_v1_n3_e64.hip": PHI,
                "futbol_v0.hip": os.environ.get("FUTBOL_PHI_FOLD_V0", "50")}  # v0: 50 measured best (-1.9%)
+# diagnostic variants: FUTBOL_PHI_EXTRA="futbol_v1_n5_e64.hip ..." builds those TUs with the threshold too
+for _src in os.environ.get("FUTBOL_PHI_EXTRA", "").split():
+    PHI_SOURCES[_src] = PHI
 
 
 def _phi_flags(src):

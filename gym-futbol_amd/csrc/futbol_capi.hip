@@ -324,7 +324,7 @@ extern "C" int futbol_create(const FutbolConfig* cfg, int32_t device, uint64_t s
         s.stamps = ctx->d_stamps;
 #endif
         int rc = launch_v1(N, ctx->epw, ctx->v1_def, (const V1Params*)ctx->d_params, B, s, 0, 1, nullptr, nullptr, nullptr,
-                           nullptr, nullptr, nullptr, 1, 0);
+                           nullptr, nullptr, nullptr, 1, 1, 0);
         if (rc) return bail(hipGetLastError(), "launch(init)");
     } else {
         V0Params hp;
@@ -342,7 +342,7 @@ extern "C" int futbol_create(const FutbolConfig* cfg, int32_t device, uint64_t s
         s.stat_cnt = (uint32_t*)fptr("stat_cnt");
         s.invalid = ctx->d_invalid;
         int rc = launch_v0((const V0Params*)ctx->d_params, B, s, 0, 1, nullptr, nullptr, nullptr, nullptr, nullptr,
-                           nullptr, 1, 0);
+                           nullptr, 1, 1, 0);
         if (rc) return bail(hipGetLastError(), "launch(init)");
     }
     if ((he = hipDeviceSynchronize()) != hipSuccess) return bail(he, "init kernel");
@@ -423,7 +423,7 @@ extern "C" int futbol_kernel_timing(FutbolCtx* ctx, int32_t mode, double* total_
 }
 
 static int launch(FutbolCtx* ctx, int what, const uint8_t* actions, const uint8_t* mask, void* obs, void* reward,
-                  uint8_t* done, void* term, void* stream)
+                  uint8_t* done, void* term, void* stream, int nsteps = 1)
 {
     FB_CHECK_HIP(ctx, hipSetDevice(ctx->device));
     const int out64 = ctx->cfg.out_dtype == FUTBOL_F64;
@@ -436,10 +436,10 @@ static int launch(FutbolCtx* ctx, int what, const uint8_t* actions, const uint8_
     int rc;
     if (ctx->cfg.env_kind == FUTBOL_ENV_V1)
         rc = launch_v1(ctx->N, ctx->epw, ctx->v1_def, (const V1Params*)ctx->d_params, ctx->B, ctx->v1, out64, what, actions,
-                       mask, obs, reward, done, term, 0, (hipStream_t)stream);
+                       mask, obs, reward, done, term, 0, nsteps, (hipStream_t)stream);
     else
         rc = launch_v0((const V0Params*)ctx->d_params, ctx->B, ctx->v0, out64, what, actions, mask, obs, reward,
-                       done, term, 0, (hipStream_t)stream);
+                       done, term, 0, nsteps, (hipStream_t)stream);
     g_launch_events = LaunchEvents{};
     if (rc) {
         hipError_t e = hipGetLastError();
@@ -461,6 +461,17 @@ extern "C" int futbol_step(FutbolCtx* ctx, const uint8_t* actions, void* obs, vo
     if (!actions || !obs || !reward || !done) return fail(ctx, FUTBOL_EINVAL, "null buffer");
     int rc = launch(ctx, 0, actions, nullptr, obs, reward, done, terminal_obs, stream);
     if (rc == FUTBOL_OK) ctx->steps_since_clear += (double)ctx->B;
+    return rc;
+}
+
+extern "C" int futbol_rollout(FutbolCtx* ctx, const uint8_t* actions, int32_t nsteps, void* obs, void* reward,
+                              uint8_t* done, void* terminal_obs, void* stream)
+{
+    if (!ctx) return FUTBOL_EINVAL;
+    if (!actions || !obs || !reward || !done) return fail(ctx, FUTBOL_EINVAL, "null buffer");
+    if (nsteps <= 0) return fail(ctx, FUTBOL_EINVAL, "nsteps must be > 0");
+    int rc = launch(ctx, 0, actions, nullptr, obs, reward, done, terminal_obs, stream, nsteps);
+    if (rc == FUTBOL_OK) ctx->steps_since_clear += (double)ctx->B * nsteps;
     return rc;
 }
 

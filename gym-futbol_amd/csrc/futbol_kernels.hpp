@@ -74,17 +74,18 @@ inline void launch_kernel(void (*k)(KArgs...), dim3 grid, dim3 block, hipStream_
         hipLaunchKernelGGL(k, grid, block, 0, stream, static_cast<KArgs>(args)...);
 }
 
-// P: device pointer to the context's V1Params (wave-uniform scalar loads)
+// P: device pointer to the context's V1Params (wave-uniform scalar loads).  what 0 = step (nsteps
+// consecutive steps per launch: the open-loop rollout, futbol_rollout), 1 = reset
 int launch_v1(int N, int epw, int def, const V1Params* P, int B, const V1Ptrs& st, int out64, int what,
               const uint8_t* actions, const uint8_t* mask, void* obs, void* reward, uint8_t* done, void* term,
-              int init, hipStream_t stream);
+              int init, int nsteps, hipStream_t stream);
 int v1_supported(int N);
 int v1_supported_epw(int epw);
 size_t v1_spill_slots(int N);
 bool v1_is_default_geometry(int N, const V1Params& p);
 
 int launch_v0(const V0Params* P, int B, const V0Ptrs& st, int out64, int what, const uint8_t* actions,
-              const uint8_t* mask, void* obs, void* reward, uint8_t* done, void* term, int init,
+              const uint8_t* mask, void* obs, void* reward, uint8_t* done, void* term, int init, int nsteps,
               hipStream_t stream);
 
 int launch_fill_actions(uint64_t seed, uint64_t step, unsigned long long* step_ctr, uint32_t env_base, int B,

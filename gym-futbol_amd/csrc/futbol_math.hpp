@@ -306,8 +306,10 @@ __host__ __device__ inline uint64_t f64_to_bits(double d)
     return u;
 }
 
-// glibc's pow(x, 2.0) computed in full (log_inline, y * log, exp_inline), |x| normal
-__host__ __device__ __attribute__((noinline)) inline double glibc_pow2_full(double x)
+// glibc's pow(x, 2.0) computed in full (log_inline, y * log, exp_inline), |x| normal.  The tables
+// may be a copy (a kernel stages them in LDS: the two dependent lookups are most of the latency)
+__host__ __device__ __forceinline__ double glibc_pow2_full(double x, const double* kPowLog = futbol::kPowLog,
+                                                          const uint64_t* kPowExp = futbol::kPowExp)
 {
     const uint64_t ix = f64_to_bits(x) & 0x7fffffffffffffffull;  // y even: pow(-x, 2) = pow(x, 2)
     const uint32_t topx = (uint32_t)(ix >> 52);
@@ -352,17 +354,66 @@ __host__ __device__ __attribute__((noinline)) inline double glibc_pow2_full(doub
     return fma(t, scale, scale);
 }
 
-// glibc pow(x, 2.0): x*x unless x^2 is within 2^-6 ulp of a rounding midpoint
-__host__ __device__ __forceinline__ double glibc_pow2(double x)
+// x*x is glibc's pow(x, 2.0) unless x^2 lies within 2^-6 ulp of a rounding midpoint (glibc's
+// pre-rounding error is below 0.0097 ulp: 1e8 samples, and 1.11 / 128 ulp + poly error by its own
+// bound); h = x*x, l = fma(x, x, -h) its exact rounding error
+__host__ __device__ __forceinline__ bool pow2_near_midpoint(double h, double l)
 {
-    const double h = x * x;
-    const double l = fma(x, x, -h);  // exact: x^2 = h + l, |l| <= ulp(h) / 2
     // ulp(h) / 2 * (1 - 2^-5) = 2^(e - 53) * (1 - 2^-5), e the exponent of h (h normal, e >= -969:
     // smaller squares go to the full path, which returns x*x for them)
     const uint64_t eb = f64_to_bits(h) & 0x7ff0000000000000ull;
     const double near = bits_to_f64(eb > (54ull << 52) ? eb - (53ull << 52) : 0ull) * (1.0 - 0x1.0p-5);
-    if (__builtin_expect(!(__builtin_fabs(l) < near), 0) && h != 0.0) return glibc_pow2_full(x);
+    return !(__builtin_fabs(l) < near) && h != 0.0;
+}
+
+// glibc pow(x, 2.0)
+__host__ __device__ __forceinline__ double glibc_pow2(double x)
+{
+    const double h = x * x;
+    if (__builtin_expect(pow2_near_midpoint(h, fma(x, x, -h)), 0)) return glibc_pow2_full(x);
     return h;
+}
+
+// glibc pow(x, 2.0) + glibc pow(y, 2.0) (get_vec's `vec[0]**2 + vec[1]**2`).  In a wave64 some lane
+// nearly always needs the slow path at a given call site (~3% per square), so the slow rounds of
+// glibc_pow2_batch (below) are each site's real cost; batch independent squares where possible
+template <int M>
+__host__ __device__ __forceinline__ void glibc_pow2_batch(const double (&x)[M], double (&h)[M], const double* logt,
+                                                         const uint64_t* expt);
+__host__ __device__ __forceinline__ double glibc_sq2(double x, double y, const double* logt = kPowLog,
+                                                    const uint64_t* expt = kPowExp)
+{
+    const double xs[2] = {x, y};
+    double h[2];
+    glibc_pow2_batch<2>(xs, h, logt, expt);
+    return h[0] + h[1];
+}
+
+// h[i] = glibc pow(x[i], 2.0) for M independent squares: x*x everywhere, then the exact glibc
+// computation for the near-midpoint ones, one per lane per round (each lane takes its lowest
+// pending square), so a wave runs max-over-lanes(pending) rounds -- nearly always one -- instead
+// of one slow branch per square.  Compile-time indices only (registers, no scratch).
+template <int M>
+__host__ __device__ __forceinline__ void glibc_pow2_batch(const double (&x)[M], double (&h)[M], const double* logt,
+                                                         const uint64_t* expt)
+{
+    static_assert(M <= 32, "pending mask");
+    uint32_t pend = 0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+        h[i] = x[i] * x[i];
+        pend |= pow2_near_midpoint(h[i], fma(x[i], x[i], -h[i])) ? 1u << i : 0u;
+    }
+    while (__builtin_expect(pend != 0u, 0)) {
+        const uint32_t bit = pend & (0u - pend);
+        double v = 0.0;
+#pragma unroll
+        for (int i = 0; i < M; ++i) v = bit == (1u << i) ? x[i] : v;
+        const double f = glibc_pow2_full(v, logt, expt);
+#pragma unroll
+        for (int i = 0; i < M; ++i) h[i] = bit == (1u << i) ? f : h[i];
+        pend &= pend - 1u;
+    }
 }
 
 }  // namespace futbol

@@ -39,13 +39,36 @@ struct Env {
     double shot_cs, shot_sn, shot_mag, shot_acc;
 };
 
+// glibc pow(x, 2.0)'s tables (futbol_powtab.h), staged in LDS by every step launch: the near-midpoint
+// squares (glibc_sq2) look them up twice in dependent succession, and some lane of a wave needs that
+// at nearly every get_vec
+__shared__ double s_pow_log[128 * 3];
+__shared__ uint64_t s_pow_exp[256];
+
+__device__ __forceinline__ void stage_pow_tables()
+{
+    for (int k = threadIdx.x; k < 128 * 3; k += 64) s_pow_log[k] = kPowLog[k];
+    for (int k = threadIdx.x; k < 256; k += 64) s_pow_exp[k] = kPowExp[k];
+    __syncthreads();
+}
+
 // get_vec (:62-65): vector from o to t and its magnitude; `vec[0]**2` is numpy's float64 power,
-// i.e. libm pow(x, 2.0) (glibc_pow2, futbol_math.hpp)
+// i.e. libm pow(x, 2.0) (glibc_sq2, futbol_math.hpp)
 __device__ __forceinline__ double get_vec(double tx, double ty, double ox, double oy, double& vx, double& vy)
 {
     vx = tx - ox;
     vy = ty - oy;
-    return sqrt(glibc_pow2(vx) + glibc_pow2(vy));
+    return sqrt(glibc_sq2(vx, vy, s_pow_log, s_pow_exp));
+}
+// two independent get_vec magnitudes, their four squares in one glibc_pow2_batch
+__device__ __forceinline__ void get_mag2(double t1x, double t1y, double o1x, double o1y, double t2x, double t2y,
+                                         double o2x, double o2y, double& m1, double& m2)
+{
+    const double d[4] = {t1x - o1x, t1y - o1y, t2x - o2x, t2y - o2y};
+    double q[4];
+    glibc_pow2_batch<4>(d, q, s_pow_log, s_pow_exp);
+    m1 = sqrt(q[0] + q[1]);
+    m2 = sqrt(q[2] + q[3]);
 }
 
 __device__ __forceinline__ double intercept_chance(double d) /* :122-129, d1 = 1, d2 = 2 */
@@ -79,9 +102,8 @@ __device__ __forceinline__ int defence_near(const Ctx& c, const Env& e)
         vy = e.vw[2 * a + 1];
     }
     constexpr int o = a < 2 ? 2 : 0;
-    double t0, t1;
-    const double d1 = get_vec(e.r[o][0], e.r[o][1], vx, vy, t0, t1);
-    const double d2 = get_vec(e.r[o + 1][0], e.r[o + 1][1], vx, vy, t0, t1);
+    double d1, d2;
+    get_mag2(e.r[o][0], e.r[o][1], vx, vy, e.r[o + 1][0], e.r[o + 1][1], vx, vy, d1, d2);
     if (d1 <= 2 && d2 <= 2) return 2;  // bigger_than (:76-82)
     if (d1 > 2 && d2 > 2) return 0;
     return 1;
@@ -197,9 +219,8 @@ __device__ __forceinline__ int get_action_type(const Ctx& c, const Env& e, bool 
     const double* ag = e.r[a];
     const double* mate = e.r[MATE[a]];
     const double* ball = e.r[BALL];
-    double t0, t1;
-    const double btam = get_vec(ball[0], ball[1], ag[0], ag[1], t0, t1);
-    const double mtam = get_vec(mate[0], mate[1], ag[0], ag[1], t0, t1);
+    double btam, mtam;
+    get_mag2(ball[0], ball[1], ag[0], ag[1], mate[0], mate[1], ag[0], ag[1], btam, mtam);
     const double shoot_x = right ? 0.0 + 20 : c.P->length - 20;
     if (has_ball) {
         if ((right && ag[0] <= shoot_x) || (!right && ag[0] >= shoot_x)) return SHOOT;
@@ -214,10 +235,18 @@ __device__ __forceinline__ int get_action_type(const Ctx& c, const Env& e, bool 
 }
 
 // _step_by_observation (:560-571); DECELERATION = 0
+__device__ __forceinline__ void step_by_observation_mag(double* o, double mag)
+{
+    const double tx = o[2], ty = o[3];
+    if (mag != 0) {
+        o[0] = o[0] + o[4] * (tx * STEP_SIZE / mag);
+        o[1] = o[1] + o[4] * (ty * STEP_SIZE / mag);
+    }
+}
 __device__ __forceinline__ void step_by_observation(double* o)
 {
     const double tx = o[2], ty = o[3];
-    const double mag = sqrt(glibc_pow2(tx) + glibc_pow2(ty));
+    const double mag = sqrt(glibc_sq2(tx, ty, s_pow_log, s_pow_exp));
     if (mag != 0) {
         o[0] = o[0] + o[4] * (tx * STEP_SIZE / mag);
         o[1] = o[1] + o[4] * (ty * STEP_SIZE / mag);
@@ -281,9 +310,9 @@ __device__ __forceinline__ void opp_team(const Ctx& c, Env& e)
 #pragma unroll
         for (int f = 0; f < 5; ++f) nb[f] = e.r[BALL][f];
         step_by_observation(nb);
-        double v1x, v1y, v2x, v2y;
-        const double m1 = get_vec(nb[0], nb[1], o1[0], o1[1], v1x, v1y);
-        const double m2 = get_vec(nb[0], nb[1], o2[0], o2[1], v2x, v2y);
+        const double v1x = nb[0] - o1[0], v1y = nb[1] - o1[1], v2x = nb[0] - o2[0], v2y = nb[1] - o2[1];
+        double m1, m2;
+        get_mag2(nb[0], nb[1], o1[0], o1[1], nb[0], nb[1], o2[0], o2[1], m1, m2);
         // selects rather than if / else-if: the branchy form lets the compiler sink the three
         // stores behind a select of row pointers, which demotes those rows to scratch
         const bool u1 = m1 < STEP_SIZE * P->player_speed, u2 = !u1 && m2 < STEP_SIZE * P->player_speed;
@@ -310,9 +339,8 @@ __device__ __forceinline__ bool score(const Env& e) /* :580-583 */
 __device__ __forceinline__ double get_reward(const V0Params* P, const Env& e, const double* ob, const double* oa1,
                                              const double* oa2, const double* oown, int act1, int act2)
 {
-    double t0, t1;
-    const double b2a1 = get_vec(ob[0], ob[1], oa1[0], oa1[1], t0, t1);
-    const double b2a2 = get_vec(ob[0], ob[1], oa2[0], oa2[1], t0, t1);
+    double b2a1, b2a2;
+    get_mag2(ob[0], ob[1], oa1[0], oa1[1], ob[0], ob[1], oa2[0], oa2[1], b2a1, b2a2);
     const double running_r = (act1 == RUN || act2 == RUN) ? 10 * 0.2 : 0;
     const double player_adv_r = ((oown[0] == 10 && act2 == RUN) || (oown[1] == 10 && act1 == RUN)) ? 10 * 0.2 : 0;
     double bad1, bad2;
@@ -423,10 +451,10 @@ using namespace v0;
 
 // FutbolEnv.step (:628-717) + DummyVecEnv auto-reset
 template <typename OT>
-__global__ void __launch_bounds__(64) v0_step_kernel(const V0Params* __restrict__ P, V0Ptrs st,
-                                                     const uint8_t* __restrict__ actions, OT* __restrict__ obs,
-                                                     OT* __restrict__ reward, uint8_t* __restrict__ done_out,
-                                                     OT* __restrict__ term_obs)
+__device__ __forceinline__ void v0_step_body(const V0Params* __restrict__ P, const V0Ptrs& st,
+                                             const uint8_t* __restrict__ actions, OT* __restrict__ obs,
+                                             OT* __restrict__ reward, uint8_t* __restrict__ done_out,
+                                             OT* __restrict__ term_obs)
 {
     const int env = blockIdx.x * 64 + threadIdx.x;
     const int B = P->B;
@@ -477,8 +505,18 @@ __global__ void __launch_bounds__(64) v0_step_kernel(const V0Params* __restrict_
     set_vector_observation<AI_1>(c, e, e.owner == AI_1, a0, false, 0, 0);
     set_vector_observation<AI_2>(c, e, e.owner == AI_2, a1, false, 0, 0);
     resolve_shot(e, rs);
+    {   // _step_vector_observations + the ball's _step_by_observation: the five magnitudes are
+        // independent, so their squares go through one glibc_pow2_batch
+        double d[10], sq[10];
 #pragma unroll
-    for (int r = 0; r < 5; ++r) step_by_observation(e.r[r]);
+        for (int r = 0; r < 5; ++r) {
+            d[2 * r] = e.r[r][2];
+            d[2 * r + 1] = e.r[r][3];
+        }
+        glibc_pow2_batch<10>(d, sq, s_pow_log, s_pow_exp);
+#pragma unroll
+        for (int r = 0; r < 5; ++r) step_by_observation_mag(e.r[r], sqrt(sq[2 * r] + sq[2 * r + 1]));
+    }
 
     const double rw = get_reward(P, e, ob, oa1, oa2, oown, a0, a1);
     bool done = false;
@@ -543,6 +581,21 @@ __global__ void __launch_bounds__(64) v0_step_kernel(const V0Params* __restrict_
     store(st, env, B, e, m, row_valid);
 }
 
+// nsteps > 1: open-loop rollout (futbol_rollout), step k on the k-th [B][...] slice of every buffer
+template <typename OT>
+__global__ void __launch_bounds__(64) v0_step_kernel(const V0Params* __restrict__ P, V0Ptrs st,
+                                                     const uint8_t* __restrict__ actions, OT* __restrict__ obs,
+                                                     OT* __restrict__ reward, uint8_t* __restrict__ done_out,
+                                                     OT* __restrict__ term_obs, int nsteps)
+{
+    stage_pow_tables();
+    const size_t B = (size_t)P->B, adim = P->action_as_int ? 1 : 2;
+#pragma unroll 1
+    for (int k = 0; k < nsteps; ++k)
+        v0_step_body<OT>(P, st, actions + (size_t)k * B * adim, obs + (size_t)k * B * 30, reward + (size_t)k * B,
+                         done_out + (size_t)k * B, term_obs ? term_obs + (size_t)k * B * 30 : nullptr);
+}
+
 template <typename OT>
 __global__ void __launch_bounds__(64) v0_reset_kernel(const V0Params* __restrict__ P, V0Ptrs st,
                                                       const uint8_t* __restrict__ mask, OT* __restrict__ obs,
@@ -579,16 +632,17 @@ __global__ void __launch_bounds__(64) v0_reset_kernel(const V0Params* __restrict
 }
 
 int launch_v0(const V0Params* P, int B, const V0Ptrs& st, int out64, int what, const uint8_t* actions,
-              const uint8_t* mask, void* obs, void* reward, uint8_t* done, void* term, int init, hipStream_t stream)
+              const uint8_t* mask, void* obs, void* reward, uint8_t* done, void* term, int init, int nsteps,
+              hipStream_t stream)
 {
     const dim3 grid((B + 63) / 64), block(64);
     if (what == 0) {
         if (out64)
             launch_kernel(v0_step_kernel<double>, grid, block, stream, P, st, actions, (double*)obs,
-                               (double*)reward, done, (double*)term);
+                          (double*)reward, done, (double*)term, nsteps);
         else
             launch_kernel(v0_step_kernel<float>, grid, block, stream, P, st, actions, (float*)obs,
-                               (float*)reward, done, (float*)term);
+                          (float*)reward, done, (float*)term, nsteps);
     } else {
         if (out64)
             hipLaunchKernelGGL((v0_reset_kernel<double>), grid, block, 0, stream, P, st, mask, (double*)obs, init);

@@ -8,7 +8,7 @@ namespace futbol {
 #define FUTBOL_DECL(n)                                                                                    \
     int launch_v1_n##n##_e64(const V1Params* P, int B, const V1Ptrs& st, int out64, int what, int def,     \
                              const uint8_t* a, const uint8_t* mask, void* obs, void* reward, uint8_t* done, \
-                             void* term, int init, hipStream_t stream);
+                             void* term, int init, int nsteps, hipStream_t stream);
 FUTBOL_DECL(1)
 FUTBOL_DECL(2)
 FUTBOL_DECL(3)
@@ -23,13 +23,14 @@ FUTBOL_DECL(10)
 
 int launch_v1(int N, int epw, int def, const V1Params* P, int B, const V1Ptrs& st, int out64, int what,
               const uint8_t* actions, const uint8_t* mask, void* obs, void* reward, uint8_t* done, void* term,
-              int init, hipStream_t stream)
+              int init, int nsteps, hipStream_t stream)
 {
     if (epw != 64) return -2;
     switch (N) {
 #define FUTBOL_CASE(n)                                                                                    \
     case n:                                                                                               \
-        return launch_v1_n##n##_e64(P, B, st, out64, what, def, actions, mask, obs, reward, done, term, init, stream);
+        return launch_v1_n##n##_e64(P, B, st, out64, what, def, actions, mask, obs, reward, done, term, init, nsteps, \
+                                    stream);
     FUTBOL_CASE(1) FUTBOL_CASE(2) FUTBOL_CASE(3) FUTBOL_CASE(4) FUTBOL_CASE(5)
     FUTBOL_CASE(6) FUTBOL_CASE(7) FUTBOL_CASE(8) FUTBOL_CASE(9) FUTBOL_CASE(10)
 #undef FUTBOL_CASE

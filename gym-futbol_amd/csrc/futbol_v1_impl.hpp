@@ -33,7 +33,6 @@
 #include <type_traits>
 #include "futbol_kernels.hpp"
 #include "futbol_v1_params.hpp"
-#include "futbol_math.hpp"
 #include "futbol_rng.hpp"
 #include "futbol_state.hpp"
 #include "futbol_util.hpp"
@@ -872,8 +871,7 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
         constexpr int k = K;
         e.vx[k] = e.vx[k] * damping + 0.0 * dt;
         e.vy[k] = e.vy[k] * damping + 0.0 * dt;
-        // the callback's l = Vec2d.length = sqrt(x**2 + y**2): Python pow squares (glibc_pow2)
-        const double s2 = glibc_pow2(e.vx[k]) + glibc_pow2(e.vy[k]);
+        const double s2 = e.vx[k] * e.vx[k] + e.vy[k] * e.vy[k];
         const double thr = k == S::BALL ? P.clamp2_ball : P.clamp2_player;
         if (s2 > thr) {
             constexpr double vmax = k == S::BALL ? kBallVmax : kPlayerVmax;
@@ -1572,7 +1570,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
     sfor<N>([&](auto I) {
         constexpr int i = I;
         const double dx = e.px[i] - e.px[BL], dy = e.py[i] - e.py[BL];
-        d0[i] = sqrt(glibc_pow2(dx) + glibc_pow2(dy));  // math.sqrt((px-bx)**2 + (py-by)**2)
+        d0[i] = sqrt(dx * dx + dy * dy);
     });
     const double bix = e.px[BL], biy = e.py[BL];
 
@@ -1619,7 +1617,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
         const double ox = press ? e.px[k] : e.px[BL], oy = press ? e.py[k] : e.py[BL];
         const double qx = press ? e.px[BL] : (shoot ? gx : tx), qy = press ? e.py[BL] : (shoot ? gy : ty);
         const double dx = qx - ox, dy = qy - oy;
-        const double mag = sqrt(glibc_pow2(dx) + glibc_pow2(dy));  // get_vec (:56-59): Python `**2`
+        const double mag = sqrt(dx * dx + dy * dy);
         const double S = press ? 40.0 : (shoot ? 120.0 : 100.0);
         const double fdx = S * dx / mag, fdy = S * dy / mag;
         // player velocity: move impulse (f * arrow) / m, or the press impulse
@@ -1719,7 +1717,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
                 sfor<N>([&](auto I) {
                     constexpr int i = I;
                     const double dx = e.px[i] - e.px[BL], dy = e.py[i] - e.py[BL];
-                    const double diff = d0[i] - sqrt(glibc_pow2(dx) + glibc_pow2(dy));
+                    const double diff = d0[i] - sqrt(dx * dx + dy * dy);
                     if constexpr (N == 5) {
                         if constexpr (i == 3) mx = diff;
                         if constexpr (i == 4) mx = diff > mx ? diff : mx;
@@ -1731,7 +1729,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
                 const double gx = W, gy = H / 2;
                 const double ax_ = e.px[BL] - gx, ay_ = e.py[BL] - gy;
                 const double ix_ = bix - gx, iy_ = biy - gy;
-                r = r + (sqrt(glibc_pow2(ix_) + glibc_pow2(iy_)) - sqrt(glibc_pow2(ax_) + glibc_pow2(ay_))) * 10;
+                r = r + (sqrt(ix_ * ix_ + iy_ * iy_) - sqrt(ax_ * ax_ + ay_ * ay_)) * 10;
             }
             // ball_contact_goal (:291-296), tested by space_step on the final positions; a goal
             // restarts from formation, the episode goes on
@@ -1780,21 +1778,34 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
 #endif
 }
 
-// DEF: the registered ids' default field (v1_default_geometry<N>), constants as immediates
+// DEF: the registered ids' default field (v1_default_geometry<N>), constants as immediates.
+// nsteps > 1: an open-loop rollout (futbol_rollout): the block's envs run nsteps consecutive
+// env-steps in one launch, step k reading actions[k] and writing obs[k] / reward[k] / done[k] /
+// term_obs[k] (each slice [B][...]); every step is the same step body with its own state load and
+// store.  Blocks never wait for each other between steps, so a wave's slow step is averaged out
+// over its own next steps instead of holding the whole grid.
 template <int N, int EPW, typename OT, bool DEF>
 __global__ void __launch_bounds__(EPW) v1_step_kernel(const V1Params* __restrict__ R, V1Ptrs st,
                                                       const uint8_t* __restrict__ actions, OT* __restrict__ obs,
                                                       OT* __restrict__ reward, uint8_t* __restrict__ done_out,
-                                                      OT* __restrict__ term_obs)
+                                                      OT* __restrict__ term_obs, int nsteps)
 {
     // 4 blocks per CU (160 KB of LDS) up to N = 7, 3 blocks beyond
     static_assert(sizeof(Scratch<N, EPW>) <= (N <= 7 ? 160 * 1024 / 4 : 160 * 1024 / 3), "LDS per block");
     __shared__ Scratch<N, EPW> sh;
-    if constexpr (DEF) {
-        constexpr V1Params G = v1_default_geometry<N>();
-        v1_step_body<N, EPW, OT>(G, R, sh, st, actions, obs, reward, done_out, term_obs);
-    } else {
-        v1_step_body<N, EPW, OT>(*R, R, sh, st, actions, obs, reward, done_out, term_obs);
+    using S = V1Shape<N>;
+    const size_t B = (size_t)R->B;
+#pragma unroll 1
+    for (int k = 0; k < nsteps; ++k) {
+        const uint8_t* a = actions + (size_t)k * B * (2 * N);
+        OT* o = obs + (size_t)k * B * (4 * S::Nb);
+        OT* t = term_obs ? term_obs + (size_t)k * B * (4 * S::Nb) : nullptr;
+        if constexpr (DEF) {
+            constexpr V1Params G = v1_default_geometry<N>();
+            v1_step_body<N, EPW, OT>(G, R, sh, st, a, o, reward + (size_t)k * B, done_out + (size_t)k * B, t);
+        } else {
+            v1_step_body<N, EPW, OT>(*R, R, sh, st, a, o, reward + (size_t)k * B, done_out + (size_t)k * B, t);
+        }
     }
 }
 

@@ -12,7 +12,7 @@
     namespace futbol {                                                                                           \
     int launch_v1_n##NP##_e64(const V1Params* P, int B, const V1Ptrs& st, int out64, int what, int def,          \
                               const uint8_t* actions, const uint8_t* mask, void* obs, void* reward, uint8_t* done, \
-                              void* term, int init, hipStream_t stream)                                          \
+                              void* term, int init, int nsteps, hipStream_t stream)                              \
     {                                                                                                            \
         constexpr int N = NP, E = 64;                                                                            \
         const dim3 grid((B + E - 1) / E), block(E);                                                              \
@@ -20,17 +20,17 @@
             if (out64) {                                                                                         \
                 if (def)                                                                                         \
                     launch_kernel(v1_step_kernel<N, E, double, true>, grid, block, stream, P, st, actions,       \
-                                  (double*)obs, (double*)reward, done, (double*)term);                           \
+                                  (double*)obs, (double*)reward, done, (double*)term, nsteps);                   \
                 else                                                                                             \
                     launch_kernel(v1_step_kernel<N, E, double, false>, grid, block, stream, P, st, actions,      \
-                                  (double*)obs, (double*)reward, done, (double*)term);                           \
+                                  (double*)obs, (double*)reward, done, (double*)term, nsteps);                   \
             } else {                                                                                             \
                 if (def)                                                                                         \
                     launch_kernel(v1_step_kernel<N, E, float, true>, grid, block, stream, P, st, actions,        \
-                                  (float*)obs, (float*)reward, done, (float*)term);                              \
+                                  (float*)obs, (float*)reward, done, (float*)term, nsteps);                      \
                 else                                                                                             \
                     launch_kernel(v1_step_kernel<N, E, float, false>, grid, block, stream, P, st, actions,       \
-                                  (float*)obs, (float*)reward, done, (float*)term);                              \
+                                  (float*)obs, (float*)reward, done, (float*)term, nsteps);                      \
             }                                                                                                    \
         } else {                                                                                                 \
             if (out64)                                                                                           \

@@ -44,6 +44,8 @@ SIGNATURES = [
     ("futbol_reset", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     ("futbol_step", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                               C.c_void_p]),
+    ("futbol_rollout", C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                 C.c_void_p]),
     ("futbol_fill_actions", C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p]),
     ("futbol_fill_actions_steps", C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_int32, C.c_void_p,
                                              C.c_void_p]),

@@ -125,6 +125,27 @@ class FutbolVecEnv:
                                              self._rew.data_ptr(), self._done.data_ptr(), self._term.data_ptr(),
                                              _stream_ptr(self.device)), self.ctx.h)
 
+    def rollout(self, actions, out=None):
+        """Open-loop rollout: K consecutive steps in one launch for actions [K, B, action_dim] (uint8,
+        device) chosen without looking at the observations.  Returns (obs [K, B, ...], reward [K, B],
+        done [K, B] (uint8), terminal_obs [K, B, ...]); slice k is what the k-th step() returns.
+        out: a tuple of such buffers to reuse (no allocation, graph-capturable)."""
+        K = int(actions.shape[0])
+        if actions.dtype != torch.uint8 or not actions.is_contiguous() or actions.device != self.device \
+                or tuple(actions.shape[1:]) != (self.num_envs, self.action_dim):
+            raise ValueError("rollout actions must be a contiguous uint8 [K, B, action_dim] tensor on the env's device")
+        if out is None:
+            out = (torch.empty((K, self.num_envs) + self.obs_shape, dtype=self.dtype, device=self.device),
+                   torch.empty((K, self.num_envs), dtype=self.dtype, device=self.device),
+                   torch.empty((K, self.num_envs), dtype=torch.uint8, device=self.device),
+                   torch.empty((K, self.num_envs) + self.obs_shape, dtype=self.dtype, device=self.device))
+        obs, rew, done, term = out
+        with torch.cuda.device(self.device):
+            nat.check(nat.load().futbol_rollout(self.ctx.h, actions.data_ptr(), K, obs.data_ptr(), rew.data_ptr(),
+                                                done.data_ptr(), term.data_ptr(), _stream_ptr(self.device)),
+                      self.ctx.h)
+        return out
+
     def random_actions(self, step, seed=1234, out=None):
         """Synthetic policy (iid uniform actions, Philox tag-1 stream), written on device."""
         out = self._act if out is None else out

@@ -96,6 +96,15 @@ int futbol_reset(FutbolCtx* ctx, const uint8_t* mask, void* obs, void* stream);
 int futbol_step(FutbolCtx* ctx, const uint8_t* actions, void* obs, void* reward, uint8_t* done,
                 void* terminal_obs, void* stream);
 
+/* Open-loop rollout: nsteps consecutive futbol_step calls in ONE launch, for callers whose actions
+   do not depend on the observations (a recorded or synthetic action sequence, a random policy).
+   actions [nsteps][B][action_dim]; obs [nsteps][B][obs_dim]; reward [nsteps][B]; done [nsteps][B];
+   terminal_obs [nsteps][B][obs_dim] or NULL -- slice k holds exactly what the k-th futbol_step call
+   would have returned (bit-identical; tested).  The envs' blocks do not wait for each other
+   between steps.  Not a reference interface: a batch-synchronous VecEnv steps with futbol_step. */
+int futbol_rollout(FutbolCtx* ctx, const uint8_t* actions, int32_t nsteps, void* obs, void* reward, uint8_t* done,
+                   void* terminal_obs, void* stream);
+
 /* Synthetic policy: actions[i] = iid uniform actions of env (env_id_base+i) at
    `step`: action j = (w * nvals) >> 32, w = word j % 4 of the Philox4x32-10 block
    (counter {j / 4, step, env id, 1}, key = seed).  step == UINT64_MAX: the

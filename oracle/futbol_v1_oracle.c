@@ -43,7 +43,7 @@
 #define SEG_RADIUS 1.0    /* futbol_env.py:187.. (last ctor arg) */
 
 /* Python's float `x**2` (libm pow in the faithful build, see oracle_math.h) */
-static double SQ(double x) { return ORC_SQ(x); }
+static double SQ(double x) { return ORC_SQ_V1(x); }
 
 /* get_vec, envs_v1/futbol_env.py:56-59: vector from o to t and its magnitude */
 static double get_vec(double tx, double ty, double ox, double oy, double *vx, double *vy)

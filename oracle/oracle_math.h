@@ -357,12 +357,18 @@ static inline double orc_glibc_pow2(double x)
 }
 
 #ifdef ORACLE_PORTABLE
-/* the kernels' arithmetic: the glibc pow(x, 2.0) and sin / cos restatements above */
+/* the kernels' arithmetic: the glibc pow(x, 2.0) and sin / cos restatements above for v0 (the
+ * reference-pinned path); envs_v1's Python-level squares (get_vec, _ball_to_team_distance_arr,
+ * pymunk's Vec2d.length) are x*x in the envs_v1 kernels -- a deliberate, measured difference from
+ * Python's pow: the v1 reference itself is unpinned, and the exact squares
+ * would cost the 2v2 step ~50% */
 #define ORC_SQ(x) orc_glibc_pow2(x)
+#define ORC_SQ_V1(x) ((x) * (x))
 #define ORC_SIN(x) orc_glibc_sin(x)
 #define ORC_COS(x) orc_glibc_cos(x)
 #else
 #define ORC_SQ(x) pow((x), 2.0)
+#define ORC_SQ_V1(x) pow((x), 2.0)
 #define ORC_SIN(x) sin(x)
 #define ORC_COS(x) cos(x)
 #endif

@@ -9,8 +9,8 @@ OUT=$R/gpurun_out/${PROF_DIR:-prof}
 mkdir -p $OUT
 hipcc --offload-arch=gfx950 -O3 -o $OUT/pmc_calib $R/scripts/pmc_calib.hip || exit 1
 cd /tmp && export TMPDIR=/tmp
-B="$R/bench.py --steps ${STEPS:-300} --warmup 20 --no-cpu-baseline --profile-steps 20 ${BENCH_ARGS:-}"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 $R/bench.py ${BENCH_ARGS:-} > $OUT/trace.log 2>&1 && \
+B="$R/bench.py --steps ${STEPS:-300} --warmup 20 --no-cpu-baseline --no-rollout-line --profile-steps 20 ${BENCH_ARGS:-}"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --no-rollout-line ${BENCH_ARGS:-} > $OUT/trace.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d $OUT/sq -o run --output-format csv -- python3 $B --graph 0 > $OUT/sq.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- python3 $B --graph 0 > $OUT/fetch.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- python3 $B --graph 0 > $OUT/write.log 2>&1 && \

@@ -274,3 +274,25 @@ def test_kernel_timing_counts_step_launches():
     tot, cnt = venv.kernel_timing(False)
     assert cnt == 25 and 0 < tot / cnt < 50.0    # ms per launch
     venv.close()
+
+
+@pytest.mark.parametrize("env_id,B,K", [("Futbol2v2-v1", 512, 350), ("Futbol5v5-v1", 128, 310), ("Futbol-v0", 256, 450)])
+def test_rollout_equals_steps(env_id, B, K):
+    """futbol_rollout (K steps in one launch, open loop) == K futbol_step calls, bit for bit, through
+    episode ends (auto-reset, terminal observations) and goals."""
+    a = gf.make(env_id, num_envs=B, seed=21)
+    b = gf.make(env_id, num_envs=B, seed=21)
+    a.reset()
+    b.reset()
+    acts = a.random_actions_steps(K, 0, seed=5)
+    obs, rew, done, term = b.rollout(acts)
+    for k in range(K):
+        o, r, d, info = a.step(acts[k])
+        assert torch.equal(o, obs[k]) and torch.equal(r, rew[k]) and torch.equal(d.to(torch.uint8), done[k]), k
+        if bool(d.any()):
+            assert torch.equal(info["terminal_observation"][d], term[k][d.bool()])
+    sa, sb = a.get_state(), b.get_state()
+    assert all(np.array_equal(sa[f], sb[f]) for f in sa)
+    assert int(done.sum()) >= B  # an episode end inside the rollout
+    a.close()
+    b.close()

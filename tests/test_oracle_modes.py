@@ -1,11 +1,17 @@
-"""Faithful (libm pow / sin / cos, = CPython) vs portable (x*x squares and the glibc sin/cos
-restatement, = the kernels) oracle builds.  The two differ only in where the libm results come
-from; tests/test_glibc_sincos.py pins the restatement against the host libm, so the builds must
-agree BIT FOR BIT on whole rollouts -- which makes the kernels' bit-exact parity with the portable
-build a bit-exact parity with the reference's own arithmetic.
+"""Faithful (libm pow / sin / cos, = CPython) vs portable (= the kernels) oracle builds.
 
-(Before round 3 the portable build used correctly rounded sin/cos, and the faithful build's
-sin(x), cos(x) pair was fused by gcc into glibc's sincos(); 1 env in ~4 000 diverged discretely.)"""
+v0: the portable build computes the reference's `x**2` and math.sin / math.cos with the glibc
+restatements (tests/test_glibc_sincos.py pins them against the host libm), so the two builds must
+agree BIT FOR BIT on whole rollouts -- the kernels' bit-exact parity with the portable build is a
+bit-exact parity with the reference's own arithmetic (and tests/test_oracle_v0.py checks it against
+1 024-env reference fingerprints).
+
+envs_v1: the kernels square with x*x where the reference's Python code writes `**2` (libm pow,
+which differs from x*x on ~0.08% of arguments): a deliberate difference,
+bounded here -- identical discrete outcomes, positions / velocities within the north star's 1e-5.
+
+(Before round 3 the faithful build was not faithful: gcc turned pow(x, 2.0) into x*x and fused
+sin(x), cos(x) into glibc's sincos(); -fno-builtin-pow/-sin/-cos/-sincos now keep libm's calls.)"""
 import numpy as np
 import pytest
 
@@ -24,8 +30,8 @@ def test_v1_faithful_vs_portable(n):
         oa, ra, da, _ = a.step(act)
         ob, rb, db, _ = b.step(act)
         assert np.array_equal(da, db)
-        assert np.array_equal(ra.view(np.uint64), rb.view(np.uint64))
-        assert np.array_equal(oa.view(np.uint64), ob.view(np.uint64))
+        assert np.array_equal(np.abs(ra) > 500, np.abs(rb) > 500)  # goals identical
+        assert np.abs(oa - ob).max() <= 1e-5 and np.abs(ra - rb).max() <= 1e-6
 
 
 @pytest.mark.parametrize("random_opp", [False, True])
