@@ -1783,9 +1783,14 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
 // env-steps in one launch, step k reading actions[k] and writing obs[k] / reward[k] / done[k] /
 // term_obs[k] (each slice [B][...]); every step is the same step body with its own state load and
 // store.  Blocks never wait for each other between steps, so a wave's slow step is averaged out
-// over its own next steps instead of holding the whole grid.
-template <int N, int EPW, typename OT, bool DEF>
-__global__ void __launch_bounds__(EPW) v1_step_kernel(const V1Params* __restrict__ R, V1Ptrs st,
+// over its own next steps instead of holding the whole grid.  ROLL = false (futbol_step): one step
+// and no loop around the body (the loop measured +7% on the 2v2 step: 21.4 -> 22.9 us).
+// experiments only: e.g. -DFUTBOL_V1_STEP_ATTR="__attribute__((amdgpu_waves_per_eu(2)))"
+#ifndef FUTBOL_V1_STEP_ATTR
+#define FUTBOL_V1_STEP_ATTR
+#endif
+template <int N, int EPW, typename OT, bool DEF, bool ROLL>
+__global__ void __launch_bounds__(EPW) FUTBOL_V1_STEP_ATTR v1_step_kernel(const V1Params* __restrict__ R, V1Ptrs st,
                                                       const uint8_t* __restrict__ actions, OT* __restrict__ obs,
                                                       OT* __restrict__ reward, uint8_t* __restrict__ done_out,
                                                       OT* __restrict__ term_obs, int nsteps)
@@ -1794,6 +1799,15 @@ __global__ void __launch_bounds__(EPW) v1_step_kernel(const V1Params* __restrict
     static_assert(sizeof(Scratch<N, EPW>) <= (N <= 7 ? 160 * 1024 / 4 : 160 * 1024 / 3), "LDS per block");
     __shared__ Scratch<N, EPW> sh;
     using S = V1Shape<N>;
+    if constexpr (!ROLL) {
+        if constexpr (DEF) {
+            constexpr V1Params G = v1_default_geometry<N>();
+            v1_step_body<N, EPW, OT>(G, R, sh, st, actions, obs, reward, done_out, term_obs);
+        } else {
+            v1_step_body<N, EPW, OT>(*R, R, sh, st, actions, obs, reward, done_out, term_obs);
+        }
+        return;
+    }
     const size_t B = (size_t)R->B;
 #pragma unroll 1
     for (int k = 0; k < nsteps; ++k) {

@@ -8,6 +8,25 @@
 #pragma once
 #include "futbol_v1_impl.hpp"
 
+namespace futbol {
+// the step kernel instance for the output type / geometry / rollout flags (ROLL: nsteps > 1)
+template <int N, typename OT>
+inline void launch_v1_step(const V1Params* P, int B, const V1Ptrs& st, int def, const uint8_t* actions, void* obs,
+                           void* reward, uint8_t* done, void* term, int nsteps, hipStream_t stream)
+{
+    constexpr int E = 64;
+    const dim3 grid((B + E - 1) / E), block(E);
+    OT *o = (OT*)obs, *r = (OT*)reward, *t = (OT*)term;
+    if (nsteps > 1) {
+        if (def) launch_kernel(v1_step_kernel<N, E, OT, true, true>, grid, block, stream, P, st, actions, o, r, done, t, nsteps);
+        else launch_kernel(v1_step_kernel<N, E, OT, false, true>, grid, block, stream, P, st, actions, o, r, done, t, nsteps);
+    } else {
+        if (def) launch_kernel(v1_step_kernel<N, E, OT, true, false>, grid, block, stream, P, st, actions, o, r, done, t, 1);
+        else launch_kernel(v1_step_kernel<N, E, OT, false, false>, grid, block, stream, P, st, actions, o, r, done, t, 1);
+    }
+}
+}  // namespace futbol
+
 #define FUTBOL_V1_INSTANCE(NP)                                                                                   \
     namespace futbol {                                                                                           \
     int launch_v1_n##NP##_e64(const V1Params* P, int B, const V1Ptrs& st, int out64, int what, int def,          \
@@ -17,21 +36,8 @@
         constexpr int N = NP, E = 64;                                                                            \
         const dim3 grid((B + E - 1) / E), block(E);                                                              \
         if (what == 0) {                                                                                         \
-            if (out64) {                                                                                         \
-                if (def)                                                                                         \
-                    launch_kernel(v1_step_kernel<N, E, double, true>, grid, block, stream, P, st, actions,       \
-                                  (double*)obs, (double*)reward, done, (double*)term, nsteps);                   \
-                else                                                                                             \
-                    launch_kernel(v1_step_kernel<N, E, double, false>, grid, block, stream, P, st, actions,      \
-                                  (double*)obs, (double*)reward, done, (double*)term, nsteps);                   \
-            } else {                                                                                             \
-                if (def)                                                                                         \
-                    launch_kernel(v1_step_kernel<N, E, float, true>, grid, block, stream, P, st, actions,        \
-                                  (float*)obs, (float*)reward, done, (float*)term, nsteps);                      \
-                else                                                                                             \
-                    launch_kernel(v1_step_kernel<N, E, float, false>, grid, block, stream, P, st, actions,       \
-                                  (float*)obs, (float*)reward, done, (float*)term, nsteps);                      \
-            }                                                                                                    \
+            if (out64) launch_v1_step<N, double>(P, B, st, def, actions, obs, reward, done, term, nsteps, stream); \
+            else launch_v1_step<N, float>(P, B, st, def, actions, obs, reward, done, term, nsteps, stream);      \
         } else {                                                                                                 \
             if (out64)                                                                                           \
                 hipLaunchKernelGGL((v1_reset_kernel<N, E, double>), grid, block, 0, stream, P, st, mask,         \

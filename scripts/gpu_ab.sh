@@ -1,12 +1,19 @@
-# A/B timing of library variants in one box: VARIANTS="old ''" (empty = the default library)
+# A/B bench lines of library variants (run via gpurun from the repo root):
+#   AB="head: main:" (variant:extra-bench-args ... ; "main" = libfutbol_amd.so)  OUT_DIR=name  PYTEST_K=expr
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out
-OUT=gpurun_out/${AB_OUT:-ab}.log; : > $OUT
-for rep in 1 2; do
-  for v in ${VARIANTS:-old default}; do
-    vv=$v; [ "$v" = default ] && vv=""
-    FUTBOL_LIB_VARIANT=$vv timeout -k 10 200 python bench.py --no-cpu-baseline --steps 1500 ${BENCH_ARGS:-} > gpurun_out/ab_one.log 2>&1 || exit 1
-    echo "$v $(tail -1 gpurun_out/ab_one.log)" >> $OUT
-  done
+O=gpurun_out/${OUT_DIR:-ab}
+mkdir -p $O
+if [ -n "$PYTEST_K" ]; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+    -k "$PYTEST_K" > $O/pytest.log 2>&1 || { echo pytest failed; exit 1; }
+fi
+i=0
+for spec in $AB; do
+  v=${spec%%:*}; args=${spec#*:}; args=${args//,/ }
+  i=$((i+1))
+  if [ "$v" = main ]; then lv=""; else lv=$v; fi
+  FUTBOL_LIB_VARIANT=$lv timeout -k 10 300 python bench.py --no-cpu-baseline --no-rollout-line $args > $O/b${i}_$v.log 2>&1 || { echo bench $spec failed; exit 1; }
+  echo "$spec $(grep -o '"value": [0-9.e+]*' $O/b${i}_$v.log) $(grep -o '"kernel_ms": [0-9.e+-]*' $O/b${i}_$v.log)"
 done
+echo rc=0
