@@ -182,15 +182,16 @@ __host__ __device__ inline uint32_t hi_word(double x)
     return (uint32_t)(b >> 32) & 0x7fffffffu;
 }
 // the table row of |x| (u = |x| + BIG rounds |x| to a multiple of 1/128); rows 0..109
-__host__ __device__ inline const double* row(double u)
+// (tab: kSinCosTab or a copy of it, e.g. staged in LDS by a kernel)
+__host__ __device__ inline const double* row(double u, const double* tab)
 {
     uint64_t b;
     memcpy(&b, &u, 8);
     uint32_t i = (uint32_t)b;
     i = i < 110u ? i : 109u;  // |x| < 0.8555 keeps i <= 109; the clamp only bounds the address
-    return kSinCosTab + 4 * i;
+    return tab + 4 * i;
 }
-__host__ __device__ inline double do_sin(double x, double dx)
+__host__ __device__ inline double do_sin(double x, double dx, const double* tab)
 {
     if (fabs(x) < 0.126) {  // TAYLOR_SIN
         const double xx = x * x;
@@ -202,18 +203,18 @@ __host__ __device__ inline double do_sin(double x, double dx)
     }
     const double d = x <= 0 ? -dx : dx;
     const double ax = fabs(x), u = ax + BIG, xr = ax - (u - BIG);
-    const double* T = row(u);
+    const double* T = row(u, tab);
     const double xx = xr * xr;
     const double sv = xr + fma(xr * xx, fma(xx, SN5, SN3), d);
     const double cv = fma(xr, d, xx * fma(xx, fma(xx, CS6, CS4), CS2));
     const double cor = fma(sv, T[2], fma(-cv, T[0], fma(sv, T[3], T[1])));
     return copysign(T[0] + cor, x);
 }
-__host__ __device__ inline double do_cos(double x, double dx)
+__host__ __device__ inline double do_cos(double x, double dx, const double* tab)
 {
     const double d = x < 0 ? -dx : dx;
     const double ax = fabs(x), u = ax + BIG, xr = (ax - (u - BIG)) + d;
-    const double* T = row(u);
+    const double* T = row(u, tab);
     const double xx = xr * xr;
     const double sv = fma(xr * xx, fma(xx, SN5, SN3), xr);
     const double cv = xx * fma(xx, fma(xx, CS6, CS4), CS2);
@@ -235,44 +236,44 @@ __host__ __device__ inline int reduce(double x, double& a, double& da)
     a = b;
     return (int)(tb & 3u);
 }
-__host__ __device__ inline double do_sincos(double a, double da, int n)
+__host__ __device__ inline double do_sincos(double a, double da, int n, const double* tab)
 {
-    const double r = (n & 1) ? do_cos(a, da) : do_sin(a, da);
+    const double r = (n & 1) ? do_cos(a, da, tab) : do_sin(a, da, tab);
     return (n & 2) ? -r : r;
 }
 }  // namespace glibc_sincos
 
-__host__ __device__ inline double glibc_sin(double x)
+__host__ __device__ inline double glibc_sin(double x, const double* tab = kSinCosTab)
 {
     using namespace glibc_sincos;
     const uint32_t k = hi_word(x);
     if (k < 0x3e500000u) return x;
-    if (k < 0x3feb6000u) return do_sin(x, 0.0);
-    if (k < 0x400368fdu) return copysign(do_cos(HP0 - fabs(x), HP1), x);
+    if (k < 0x3feb6000u) return do_sin(x, 0.0, tab);
+    if (k < 0x400368fdu) return copysign(do_cos(HP0 - fabs(x), HP1, tab), x);
     if (k < 0x419921fbu) {
         double a, da;
         const int n = reduce(x, a, da);
-        return do_sincos(a, da, n);
+        return do_sincos(a, da, n, tab);
     }
     double sn, cs;
     cr_sincos(x, &sn, &cs);
     return sn;
 }
-__host__ __device__ inline double glibc_cos(double x)
+__host__ __device__ inline double glibc_cos(double x, const double* tab = kSinCosTab)
 {
     using namespace glibc_sincos;
     const uint32_t k = hi_word(x);
     if (k < 0x3e400000u) return 1.0;
-    if (k < 0x3feb6000u) return do_cos(x, 0.0);
+    if (k < 0x3feb6000u) return do_cos(x, 0.0, tab);
     if (k < 0x400368fdu) {
         const double y = HP0 - fabs(x);
         const double a = y + HP1;
-        return do_sin(a, (y - a) + HP1);
+        return do_sin(a, (y - a) + HP1, tab);
     }
     if (k < 0x419921fbu) {
         double a, da;
         const int n = reduce(x, a, da);
-        return do_sincos(a, da, n + 1);
+        return do_sincos(a, da, n + 1, tab);
     }
     double sn, cs;
     cr_sincos(x, &sn, &cs);
@@ -307,7 +308,9 @@ __host__ __device__ inline uint64_t f64_to_bits(double d)
 }
 
 // glibc's pow(x, 2.0) computed in full (log_inline, y * log, exp_inline), |x| normal.  The tables
-// may be a copy (a kernel stages them in LDS: the two dependent lookups are most of the latency)
+// may be a copy (a kernel stages them in LDS: the two dependent lookups are most of the latency).
+// Inlined at every site (~30 in the v0 step kernel, 80 KB of code): a non-inlined copy (850 bytes,
+// 22 VGPRs) measured 1% slower
 __host__ __device__ __forceinline__ double glibc_pow2_full(double x, const double* kPowLog = futbol::kPowLog,
                                                           const uint64_t* kPowExp = futbol::kPowExp)
 {
@@ -404,6 +407,9 @@ __host__ __device__ __forceinline__ void glibc_pow2_batch(const double (&x)[M], 
         h[i] = x[i] * x[i];
         pend |= pow2_near_midpoint(h[i], fma(x[i], x[i], -h[i])) ? 1u << i : 0u;
     }
+#ifdef FUTBOL_DIAG_PLAIN_SQ  // diagnostic builds only (cost of the exact squares): x*x, NOT glibc's
+    pend = 0u;
+#endif
     while (__builtin_expect(pend != 0u, 0)) {
         const uint32_t bit = pend & (0u - pend);
         double v = 0.0;

@@ -44,11 +44,14 @@ struct Env {
 // at nearly every get_vec
 __shared__ double s_pow_log[128 * 3];
 __shared__ uint64_t s_pow_exp[256];
+// and glibc's sin / cos table (resolve_shot: some lane of nearly every wave shoots)
+__shared__ double s_sincos[440];
 
 __device__ __forceinline__ void stage_pow_tables()
 {
     for (int k = threadIdx.x; k < 128 * 3; k += 64) s_pow_log[k] = kPowLog[k];
     for (int k = threadIdx.x; k < 256; k += 64) s_pow_exp[k] = kPowExp[k];
+    for (int k = threadIdx.x; k < 440; k += 64) s_sincos[k] = kSinCosTab[k];
     __syncthreads();
 }
 
@@ -59,6 +62,13 @@ __device__ __forceinline__ double get_vec(double tx, double ty, double ox, doubl
     vx = tx - ox;
     vy = ty - oy;
     return sqrt(glibc_sq2(vx, vy, s_pow_log, s_pow_exp));
+}
+// get_vec whose magnitude the reference discards (`vec, _ = get_vec(...)`, :348-350, :434-436,
+// :941-947): pow(x, 2.0) has no side effect, so only the vector is computed
+__device__ __forceinline__ void vec_only(double tx, double ty, double ox, double oy, double& vx, double& vy)
+{
+    vx = tx - ox;
+    vy = ty - oy;
 }
 // two independent get_vec magnitudes, their four squares in one glibc_pow2_batch
 __device__ __forceinline__ void get_mag2(double t1x, double t1y, double o1x, double o1y, double t2x, double t2y,
@@ -139,7 +149,7 @@ __device__ __forceinline__ void set_vector_observation(const Ctx& c, Env& e, boo
                 ag[3] = tgy;
             } else {
                 double vx, vy;
-                get_vec(right ? 0.0 : P->length, target_y, ag[0], ag[1], vx, vy);
+                vec_only(right ? 0.0 : P->length, target_y, ag[0], ag[1], vx, vy);
                 ag[2] = vx;
                 ag[3] = vy;
             }
@@ -185,7 +195,7 @@ __device__ __forceinline__ void set_vector_observation(const Ctx& c, Env& e, boo
     } else {
         double btax, btay, gtax, gtay;
         const double btam = get_vec(ball[0], ball[1], ag[0], ag[1], btax, btay);
-        get_vec(right ? 0.0 : P->length, P->width / 2, ag[0], ag[1], gtax, gtay);
+        vec_only(right ? 0.0 : P->length, P->width / 2, ag[0], ag[1], gtax, gtay);
         if (action == INTERCEPT) {
             const bool success = Stream::uniform01_of(blk[1]) < intercept_chance(btam);
             used = 2;
@@ -211,16 +221,14 @@ __device__ __forceinline__ void set_vector_observation(const Ctx& c, Env& e, boo
 // Easy_Agent.get_action_type (easy_agent.py:53-98), shoot_range = 20 (futbol_env.py:196-201).
 // ub: the block of the stream's current draw, computed once for both opponents by opp_team (at
 // most one of them holds the ball, so at most one draws, and at that position)
+// btam, mtam: |ball - agent| and |mate - agent|, computed with the step's first batch of squares
 template <int a>
 __device__ __forceinline__ int get_action_type(const Ctx& c, const Env& e, bool has_ball, bool team_has_ball,
-                                               const Philox4& ub)
+                                               const Philox4& ub, double btam, double mtam)
 {
     constexpr bool right = a >= 2;
     const double* ag = e.r[a];
     const double* mate = e.r[MATE[a]];
-    const double* ball = e.r[BALL];
-    double btam, mtam;
-    get_mag2(ball[0], ball[1], ag[0], ag[1], mate[0], mate[1], ag[0], ag[1], btam, mtam);
     const double shoot_x = right ? 0.0 + 20 : c.P->length - 20;
     if (has_ball) {
         if ((right && ag[0] <= shoot_x) || (!right && ag[0] >= shoot_x)) return SHOOT;
@@ -263,7 +271,7 @@ __device__ __forceinline__ void resolve_shot(Env& e, const Stream& rs)
     const double nd = Stream::normal_of(rs.block(e.shot_pos), 0.0, e.shot_acc);
     const double ang = (nd / 180) * 3.141592653589793;
     // math.sin / math.cos of the reference: glibc's (futbol_math.hpp glibc_sin / glibc_cos)
-    const double ss = glibc_sin(ang), sc = glibc_cos(ang);
+    const double ss = glibc_sin(ang, s_sincos), sc = glibc_cos(ang, s_sincos);
     const double cs = e.shot_cs, sn = e.shot_sn;
     const double tc = (cs * sc) - (sn * ss), ts = (sn * sc) + (cs * ss);
     e.r[BALL][2] = tc * e.shot_mag;
@@ -271,15 +279,16 @@ __device__ __forceinline__ void resolve_shot(Env& e, const Stream& rs)
     e.shot = false;
 }
 
-// _opp_team_set_vector_observation (:864-983)
-__device__ __forceinline__ void opp_team(const Ctx& c, Env& e)
+// _opp_team_set_vector_observation (:864-983); m3 = |ball - opp_1|, |ball - opp_2|, |opp_2 - opp_1|
+// (= |opp_1 - opp_2|: pow(-x, 2) = pow(x, 2)) of the state at the top of the step
+__device__ __forceinline__ void opp_team(const Ctx& c, Env& e, const double (&m3)[3])
 {
     const V0Params* P = c.P;
     const bool o1has = e.owner == OPP_1, o2has = e.owner == OPP_2;
     const bool team = o1has || o2has;
     const Philox4 ub = c.rs->block(c.rs->j);
-    int a1 = get_action_type<OPP_1>(c, e, o1has, team, ub);
-    int a2 = get_action_type<OPP_2>(c, e, o2has, team, ub);
+    int a1 = get_action_type<OPP_1>(c, e, o1has, team, ub, m3[0], m3[2]);
+    int a2 = get_action_type<OPP_2>(c, e, o2has, team, ub, m3[1], m3[2]);
     const int opp1_action = a1, opp2_action = a2;  // the Action enums keep the pre-override values (D.13)
     bool s1 = false, s2 = false;
     double t1x = 0, t1y = 0, t2x = 0, t2y = 0;
@@ -298,8 +307,8 @@ __device__ __forceinline__ void opp_team(const Ctx& c, Env& e)
     if (e.owner == AI_1 || e.owner == AI_2) {
         if (e.r[BALL][0] < P->length * 0.6) {
             const double dpx = P->length * 0.75, dpy = P->width * 0.5;
-            if (o1[0] > o2[0]) { a1 = RUN; s1 = true; get_vec(dpx, dpy, o1[0], o1[1], t1x, t1y); }
-            else { a2 = RUN; s2 = true; get_vec(dpx, dpy, o2[0], o2[1], t2x, t2y); }
+            if (o1[0] > o2[0]) { a1 = RUN; s1 = true; vec_only(dpx, dpy, o1[0], o1[1], t1x, t1y); }
+            else { a2 = RUN; s2 = true; vec_only(dpx, dpy, o2[0], o2[1], t2x, t2y); }
         }
     }
     set_vector_observation<OPP_1>(c, e, o1has, a1, s1, t1x, t1y);
@@ -335,12 +344,12 @@ __device__ __forceinline__ bool score(const Env& e) /* :580-583 */
     return ai_in || opp_in;
 }
 
-// _get_reward (:752-861); ob/oa1/oa2/oown: copies taken at the top of step()
+// _get_reward (:752-861); ob/oa1/oa2/oown: copies taken at the top of step(); b2a1 / b2a2 =
+// |ob - oa1| / |ob - oa2|, computed with the step's first batch of squares
 __device__ __forceinline__ double get_reward(const V0Params* P, const Env& e, const double* ob, const double* oa1,
-                                             const double* oa2, const double* oown, int act1, int act2)
+                                             const double* oa2, const double* oown, int act1, int act2,
+                                             double b2a1, double b2a2)
 {
-    double b2a1, b2a2;
-    get_mag2(ob[0], ob[1], oa1[0], oa1[1], ob[0], ob[1], oa2[0], oa2[1], b2a1, b2a2);
     const double running_r = (act1 == RUN || act2 == RUN) ? 10 * 0.2 : 0;
     const double player_adv_r = ((oown[0] == 10 && act2 == RUN) || (oown[1] == 10 && act1 == RUN)) ? 10 * 0.2 : 0;
     double bad1, bad2;
@@ -495,12 +504,34 @@ __device__ __forceinline__ void v0_step_body(const V0Params* __restrict__ P, con
         oown[f] = (row_valid_before && f == oidx) ? 10 : 0;
     }
 
+    // the magnitudes of the step's initial state, their squares in one batch: _get_reward's ball to
+    // ai_1 / ai_2 (of the copies o_b, o_ai_1, o_ai_2) and the opponents' get_action_type (hard-coded
+    // opponent: ball to opp_1 / opp_2, opp_1 to opp_2)
+    double b2a1, b2a2, m3[3];
+    {
+        const double* o1 = e.r[OPP_1];
+        const double* o2 = e.r[OPP_2];
+        const double d[10] = {ob[0] - oa1[0], ob[1] - oa1[1], ob[0] - oa2[0], ob[1] - oa2[1],
+                              ob[0] - o1[0], ob[1] - o1[1], ob[0] - o2[0], ob[1] - o2[1], o2[0] - o1[0], o2[1] - o1[1]};
+        double q[10];
+        if (P->random_opp) {
+            glibc_pow2_batch<4>(*reinterpret_cast<const double(*)[4]>(d), *reinterpret_cast<double(*)[4]>(q),
+                                s_pow_log, s_pow_exp);
+        } else {
+            glibc_pow2_batch<10>(d, q, s_pow_log, s_pow_exp);
+            m3[0] = sqrt(q[4] + q[5]);
+            m3[1] = sqrt(q[6] + q[7]);
+            m3[2] = sqrt(q[8] + q[9]);
+        }
+        b2a1 = sqrt(q[0] + q[1]);
+        b2a2 = sqrt(q[2] + q[3]);
+    }
     if (P->random_opp) {
         const int t = rs.randint(0, 15);
         set_vector_observation<OPP_1>(c, e, e.owner == OPP_1, t / 4, false, 0, 0);
         set_vector_observation<OPP_2>(c, e, e.owner == OPP_2, t % 4, false, 0, 0);
     } else {
-        opp_team(c, e);
+        opp_team(c, e, m3);
     }
     set_vector_observation<AI_1>(c, e, e.owner == AI_1, a0, false, 0, 0);
     set_vector_observation<AI_2>(c, e, e.owner == AI_2, a1, false, 0, 0);
@@ -518,7 +549,7 @@ __device__ __forceinline__ void v0_step_body(const V0Params* __restrict__ P, con
         for (int r = 0; r < 5; ++r) step_by_observation_mag(e.r[r], sqrt(sq[2 * r] + sq[2 * r + 1]));
     }
 
-    const double rw = get_reward(P, e, ob, oa1, oa2, oown, a0, a1);
+    const double rw = get_reward(P, e, ob, oa1, oa2, oown, a0, a1, b2a1, b2a2);
     bool done = false;
     if (score(e)) {
         const int who = e.r[BALL][0] <= 0 ? 1 : 0;
@@ -581,14 +612,19 @@ __device__ __forceinline__ void v0_step_body(const V0Params* __restrict__ P, con
     store(st, env, B, e, m, row_valid);
 }
 
-// nsteps > 1: open-loop rollout (futbol_rollout), step k on the k-th [B][...] slice of every buffer
-template <typename OT>
+// ROLL (nsteps > 1): open-loop rollout (futbol_rollout), step k on the k-th [B][...] slice of every
+// buffer; the single-step instance has no loop around the body
+template <typename OT, bool ROLL>
 __global__ void __launch_bounds__(64) v0_step_kernel(const V0Params* __restrict__ P, V0Ptrs st,
                                                      const uint8_t* __restrict__ actions, OT* __restrict__ obs,
                                                      OT* __restrict__ reward, uint8_t* __restrict__ done_out,
                                                      OT* __restrict__ term_obs, int nsteps)
 {
     stage_pow_tables();
+    if constexpr (!ROLL) {
+        v0_step_body<OT>(P, st, actions, obs, reward, done_out, term_obs);
+        return;
+    }
     const size_t B = (size_t)P->B, adim = P->action_as_int ? 1 : 2;
 #pragma unroll 1
     for (int k = 0; k < nsteps; ++k)
@@ -637,12 +673,21 @@ int launch_v0(const V0Params* P, int B, const V0Ptrs& st, int out64, int what, c
 {
     const dim3 grid((B + 63) / 64), block(64);
     if (what == 0) {
-        if (out64)
-            launch_kernel(v0_step_kernel<double>, grid, block, stream, P, st, actions, (double*)obs,
-                          (double*)reward, done, (double*)term, nsteps);
-        else
-            launch_kernel(v0_step_kernel<float>, grid, block, stream, P, st, actions, (float*)obs,
-                          (float*)reward, done, (float*)term, nsteps);
+        if (out64) {
+            if (nsteps > 1)
+                launch_kernel(v0_step_kernel<double, true>, grid, block, stream, P, st, actions, (double*)obs,
+                              (double*)reward, done, (double*)term, nsteps);
+            else
+                launch_kernel(v0_step_kernel<double, false>, grid, block, stream, P, st, actions, (double*)obs,
+                              (double*)reward, done, (double*)term, 1);
+        } else {
+            if (nsteps > 1)
+                launch_kernel(v0_step_kernel<float, true>, grid, block, stream, P, st, actions, (float*)obs,
+                              (float*)reward, done, (float*)term, nsteps);
+            else
+                launch_kernel(v0_step_kernel<float, false>, grid, block, stream, P, st, actions, (float*)obs,
+                              (float*)reward, done, (float*)term, 1);
+        }
     } else {
         if (out64)
             hipLaunchKernelGGL((v0_reset_kernel<double>), grid, block, 0, stream, P, st, mask, (double*)obs, init);
