@@ -142,6 +142,9 @@ constexpr bool kSolveComponents = 2 * N + 1 <= 8;
 #ifndef FUTBOL_K2
 #define FUTBOL_K2 7
 #endif
+#ifndef FUTBOL_K5
+#define FUTBOL_K5 4
+#endif
 template <int N>
 struct V1Shape {
     static constexpr int Nb = 2 * N + 1;
@@ -150,7 +153,7 @@ struct V1Shape {
     // LDS contact-record slots per lane: 4 one-wave blocks per CU must fit in 160 KB
     // (40 KB per block: K * 4 KB of records + (2 Nb + 1) KB of solver velocity rows + the segment table)
     // for N <= 7; N = 8, 9, 10 (the rows alone take 35-43 KB) fit 3 blocks per CU (53 KB each)
-    static constexpr int K = N == 1 ? 8 : (N == 2 ? FUTBOL_K2 : (N == 3 ? 6 : (N == 4 ? 5 : (N == 5 ? 4 :
+    static constexpr int K = N == 1 ? 8 : (N == 2 ? FUTBOL_K2 : (N == 3 ? 6 : (N == 4 ? 5 : (N == 5 ? FUTBOL_K5 :
                              (N == 6 ? 3 : (N == 7 ? 2 : (N == 8 ? 4 : (N == 9 ? 3 : 2))))))));
 };
 
