@@ -327,7 +327,7 @@ def main():
                           "reference_v0_python": REF_V0_PYTHON}), flush=True)
         return
     if args.stamps:
-        os.environ["FUTBOL_LIB_VARIANT"] = "stamps"
+        os.environ.setdefault("FUTBOL_LIB_VARIANT", "stamps")  # (a stamps build of another variant: set it)
 
     from gym_futbol_amd import FutbolVecEnv
     from gym_futbol_amd import distributed as D

@@ -51,9 +51,17 @@ def _phi_flags(src):
 SCHED = os.environ.get("FUTBOL_SCHED", "max-memory-clause")
 
 
+# Only the instances without scratch spills (N <= 5): the N = 9 double-output step instance
+# (512 VGPRs, ~300 spilled VGPRs, 1.3 KB of scratch per lane) computed wrong velocities on the GPU
+# with this strategy and right ones with LLVM's default scheduler or at -O1, from the same source
+# (round 3, scripts/diag_n9.py; -verify-machineinstrs reports nothing) -- a code-generation fault
+# at the register limit, like the phi-folding one of round 2 ("compiler").
+SCHED_SOURCES = {"futbol_v1_n%d_e64.hip" % n for n in (1, 2, 3, 4, 5)}
+
+
 def _sched_flags(src):
     b = os.path.basename(src)
-    if not SCHED or not (b.startswith("futbol_v1") and b.endswith(".hip")):
+    if not SCHED or b not in SCHED_SOURCES:
         return []
     return ["-mllvm", "-amdgpu-sched-strategy=" + SCHED]
 # A/B of compiler options: FUTBOL_EXTRA_CFLAGS="..." (with a FUTBOL_BUILD_VARIANT name)

@@ -434,7 +434,7 @@ __device__ __forceinline__ bool cs_hit(const V1Params& P, int s, double cx, doub
 // (every segment lies on x<=0, x>=W, y<=0 or y>=H; the test needs distance < rc+1)
 __device__ __forceinline__ bool far_from_segments(double x, double y, double reach, double W, double H)
 {
-    return x > reach && x < W - reach && y > reach && y < H - reach;
+    return (x > reach) & (x < W - reach) & (y > reach) & (y < H - reach);
 }
 
 // ---------------------------------------------------------------------------
@@ -526,7 +526,7 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
             constexpr double ri = i == S::BALL ? kBallR : kPlayerR;
             const double cl = e.px[i] - ri, cb = e.py[i] - ri, cr = e.px[i] + ri, ct = e.py[i] + ri;
             // every segment's cpBB lies within 1 of the field border: exact reject of all 12
-            const bool interior = cl > 1.0 && cr < W - 1.0 && cb > 1.0 && ct < H - 1.0;
+            const bool interior = (cl > 1.0) & (cr < W - 1.0) & (cb > 1.0) & (ct < H - 1.0);
             const BBT& T = P.bbt;
             // each of the 16 distinct bounds contributes the set of segments whose cpBB uses it;
             // a segment is a candidate when all four of its bounds hold (the AND of four sets):
@@ -579,10 +579,12 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
             constexpr int j = J;
             constexpr double rj = j == S::BALL ? kBallR : kPlayerR;
             constexpr int q = i * S::Nb - i * (i + 1) / 2 + (j - i - 1);
-            const bool bb = cl <= e.px[j] + rj && e.px[j] - rj <= cr && cb <= e.py[j] + rj && e.py[j] - rj <= ct;
+            // (non-short-circuit & : every operand is computed anyway; `&&` became a divergent
+            // branch per pair in the instances built without the phi-folding threshold, N >= 4)
+            const bool bb = (cl <= e.px[j] + rj) & (e.px[j] - rj <= cr) & (cb <= e.py[j] + rj) & (e.py[j] - rj <= ct);
             const double mind = ri + rj;
             const double dx = e.px[j] - e.px[i], dy = e.py[j] - e.py[i];
-            hpw[q / 64] |= (bb && dx * dx + dy * dy < mind * mind) ? 1ull << (q % 64) : 0ull;
+            hpw[q / 64] |= (bb & (dx * dx + dy * dy < mind * mind)) ? 1ull << (q % 64) : 0ull;
         });
     });
     FUTBOL_STAMP(dtc == 2 ? 18 : 9);
@@ -1170,7 +1172,7 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
     bool fok = goal;
     sfor<S::Nb>([&](auto K) {
         constexpr int k = K;
-        fok = fok && __builtin_fabs(e.bx[k]) < P.form_vb && __builtin_fabs(e.by[k]) < P.form_vb;
+        fok = fok & (__builtin_fabs(e.bx[k]) < P.form_vb) & (__builtin_fabs(e.by[k]) < P.form_vb);
     });
     pre_aged = fok;
     const uint32_t xa = fok ? 1u : 0u;
@@ -1245,7 +1247,7 @@ __device__ __forceinline__ bool formation_step(const V1Params& P, const Lane<N, 
     bool ok = true;
     sfor<S::Nb>([&](auto K) {
         constexpr int k = K;
-        ok = ok && __builtin_fabs(e.bx[k]) < P.form_vb && __builtin_fabs(e.by[k]) < P.form_vb;
+        ok = ok & (__builtin_fabs(e.bx[k]) < P.form_vb) & (__builtin_fabs(e.by[k]) < P.form_vb);
     });
     if (!ok) return false;
     const double dt = P.dtv[1], damping = P.damp[1];
@@ -1416,8 +1418,37 @@ __device__ __forceinline__ void do_reset(const V1Params& P, const V1Params* __re
 
 // Team.get_pass_target_teammate (team.py:136-180) for player `me` of team `side`:
 // returns the teammate's position.
+// The pass-target draws of one step's player loop (N >= 3).  A passing player (touching the ball,
+// key 4) makes one draw (random.choices over its teammates) plus one when an arrow is held and some
+// teammate lies that way, at the lane's next stream positions; no other call in the loop draws.
+// So a lane's pass draws are the consecutive positions j0, j0 + 1, ... from the loop's start, and
+// nearly every lane makes at most two (one passer per step).  Their blocks are computed once per
+// step for the whole wave, at a converged point, instead of inside each passing player's
+// divergent branch (which some lane of a 5v5 wave enters for most players: 5.6 k of the wave's
+// 96.6 k cycles per step); a draw past j0 + 1 (a second passer) computes its own block.
+// N = 3..5 (5v5 51.0 -> 50.4 us, 3v3 29.4 -> 28.6 us); 10v10 measured 2% slower with it (twenty
+// players: more lanes with a second passer, more registers), N >= 6 keeps the blocks in the branch
+template <int N>
+constexpr bool kPassDraws = N >= 3 && N <= 5;
+struct PassDraws {
+    uint32_t j0;
+    uint32_t a0, b0, a1, b1;  // words 0 and 1 of the blocks at j0 and j0 + 1 (all choice_of reads)
+    __device__ __forceinline__ int choice(Stream& rs, int n)
+    {
+        const uint32_t x = rs.j++;
+        uint32_t a = x == j0 ? a0 : a1, b = x == j0 ? b0 : b1;
+        if (x - j0 > 1u) {  // rare: a later passer of the same lane
+            const Philox4 p = rs.block(x);
+            a = p.x[0];
+            b = p.x[1];
+        }
+        const int k = (int)floor(u53(a, b) * (double)n);
+        return k > n - 1 ? n - 1 : k;
+    }
+};
+
 template <int N, int side, int me>
-__device__ __forceinline__ void pass_target(const Env<N>& e, Stream& rs, int ar, double& tx, double& ty)
+__device__ __forceinline__ void pass_target(const Env<N>& e, Stream& rs, PassDraws& pd, int ar, double& tx, double& ty)
 {
     constexpr int base = side * N;
     if constexpr (N == 1) {
@@ -1433,13 +1464,13 @@ __device__ __forceinline__ void pass_target(const Env<N>& e, Stream& rs, int ar,
             rs.skip(1);
             t = 0;
         } else {
-            t = rs.choice(N - 1);
+            t = kPassDraws<N> ? pd.choice(rs, N - 1) : rs.choice(N - 1);
         }
         t = t >= me ? t + 1 : t;
         if (ar != 0) {
             const double x0 = e.px[base + me], y0 = e.py[base + me];
             auto dir_ok = [&](double mx, double my) {
-                return (ar == 1 && my > 0) || (ar == 2 && mx > 0) || (ar == 3 && my < 0) || (ar == 4 && mx < 0);
+                return ((ar == 1) & (my > 0)) | ((ar == 2) & (mx > 0)) | ((ar == 3) & (my < 0)) | ((ar == 4) & (mx < 0));
             };
             int cnt = 0;
             sfor<N>([&](auto Q) {
@@ -1452,7 +1483,7 @@ __device__ __forceinline__ void pass_target(const Env<N>& e, Stream& rs, int ar,
                     rs.skip(1);
                     pick = 0;
                 } else {
-                    pick = rs.choice(cnt);
+                    pick = kPassDraws<N> ? pd.choice(rs, cnt) : rs.choice(cnt);
                 }
                 sfor<N>([&](auto Q) {
                     constexpr int q = Q;
@@ -1591,6 +1622,19 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
     // branch outcome is applied with exact selects (no +-0 additions) -- identical
     // results to the reference's five-way branch, without executing all of its arms.
     uint32_t owner = e.meta.owner();
+    PassDraws pd{};
+    if constexpr (kPassDraws<N>) {
+        pd.j0 = rs.j;
+        bool anyp = false;
+        sfor<2 * N>([&](auto K) { anyp = anyp | ((key[K] == 4) & touch[K]); });
+        if (__ballot(anyp)) {  // wave-uniform: both blocks for every lane of a wave with a passer
+            const Philox4 p0 = rs.block(pd.j0), p1 = rs.block(pd.j0 + 1);
+            pd.a0 = p0.x[0];
+            pd.b0 = p0.x[1];
+            pd.a1 = p1.x[0];
+            pd.b1 = p1.x[1];
+        }
+    }
     sfor<2 * N>([&](auto K) {
         constexpr int k = K;
         constexpr int side = k < N ? 0 : 1;
@@ -1599,9 +1643,9 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
         const int fx = ar == 2 ? 1 : (ar == 4 ? -1 : 0);
         const int fy = ar == 1 ? 1 : (ar == 3 ? -1 : 0);
         const bool move = ky <= 1;                      // noop / dash (:331-341)
-        const bool shoot = ky == 2 && tk;               // (:344-368)
-        const bool press = ky == 3 && !tk && ar == 0;   // (:371-391)
-        const bool pass = ky == 4 && tk;                // (:394-419)
+        const bool shoot = (ky == 2) & tk;              // (:344-368)
+        const bool press = (ky == 3) & !tk & (ar == 0); // (:371-391)
+        const bool pass = (ky == 4) & tk;               // (:394-419)
         double tx = 0.0, ty = 0.0;
         if constexpr (N == 2) {
             // one teammate: get_pass_target_teammate always returns it (team.py:136-180); its
@@ -1609,12 +1653,17 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
             // plus one when an arrow is held and the teammate lies strictly that way
             constexpr int mate = side * N + (1 - (k - side * N));
             const double mx = e.px[mate] - e.px[k], my = e.py[mate] - e.py[k];
-            const bool way = (ar == 1 && my > 0) || (ar == 2 && mx > 0) || (ar == 3 && my < 0) || (ar == 4 && mx < 0);
+            const bool way = ((ar == 1) & (my > 0)) | ((ar == 2) & (mx > 0)) | ((ar == 3) & (my < 0)) | ((ar == 4) & (mx < 0));
             tx = e.px[mate];
             ty = e.py[mate];
             rs.skip(pass ? (way ? 2u : 1u) : 0u);
         } else {
-            if (pass) pass_target<N, side, k - side * N>(e, rs, ar, tx, ty);
+#ifdef FUTBOL_DIAG_NOPASS  // diagnostic only (wrong results): the cost of the pass-target draws
+            tx = e.px[side * N];
+            ty = e.py[side * N];
+#else
+            if (pass) pass_target<N, side, k - side * N>(e, rs, pd, ar, tx, ty);
+#endif
         }
         const double gx = side == 0 ? W : 0.0, gy = H / 2;
         const double ox = press ? e.px[k] : e.px[BL], oy = press ? e.py[k] : e.py[BL];
@@ -1632,7 +1681,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
         // ball velocity: dribble (ball takes the player's velocity) or a kick (v/2 or v/10, + impulse)
         const double D = shoot ? 2.0 : 10.0, rD = shoot ? 0.5 : 0.1;
         const double kvx = cdiv(e.vx[BL], D, rD) + fdx * kBallMinv, kvy = cdiv(e.vy[BL], D, rD) + fdy * kBallMinv;
-        const bool dribble = move && tk, kick = shoot || pass;
+        const bool dribble = move & tk, kick = shoot | pass;
         e.vx[BL] = dribble ? e.vx[k] : (kick ? kvx : e.vx[BL]);
         e.vy[BL] = dribble ? e.vy[k] : (kick ? kvy : e.vy[BL]);
         owner = tk ? (uint32_t)side : owner;
