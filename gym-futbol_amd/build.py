@@ -56,7 +56,19 @@ SCHED = os.environ.get("FUTBOL_SCHED", "max-memory-clause")
 # with this strategy and right ones with LLVM's default scheduler or at -O1, from the same source
 # (round 3, scripts/diag_n9.py; -verify-machineinstrs reports nothing) -- a code-generation fault
 # at the register limit, like the phi-folding one of round 2 ("compiler").
-SCHED_SOURCES = {"futbol_v1_n%d_e64.hip" % n for n in (1, 2, 3, 4, 5)}
+# N = 3 is left out too: its rollout instances (f32 default field, f64 runtime geometry) diverged from
+# the oracle at step 19 of tests/test_gpu_instances.py with this strategy and the phi-folding
+# threshold together (either one alone: correct)
+SCHED_SOURCES = {"futbol_v1_n%d_e64.hip" % n for n in (1, 2, 4, 5)}
+
+
+# extra flags for the large instances (N = 6..10: 512 VGPRs with spills), e.g. FUTBOL_BIG_FLAGS=-O1
+BIG_SOURCES = {"futbol_v1_n%d_e64.hip" % n for n in (6, 7, 8, 9, 10)}
+BIG_FLAGS = os.environ.get("FUTBOL_BIG_FLAGS", "").split()
+
+
+def _big_flags(src):
+    return BIG_FLAGS if os.path.basename(src) in BIG_SOURCES else []
 
 
 def _sched_flags(src):
@@ -88,7 +100,7 @@ def _stale(target, sources):
 def _compile(src, force):
     obj = os.path.join(OBJ, os.path.basename(src) + ".o")
     if force or _stale(obj, [src] + _deps()):
-        cmd = [HIPCC] + CFLAGS + _phi_flags(src) + _sched_flags(src) + ["-c", src, "-o", obj]
+        cmd = [HIPCC] + CFLAGS + _phi_flags(src) + _sched_flags(src) + _big_flags(src) + ["-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("hipcc failed for %s:\n%s\n%s" % (src, " ".join(cmd), r.stderr[-8000:]))

@@ -235,7 +235,7 @@ extern "C" int futbol_create(const FutbolConfig* cfg, int32_t device, uint64_t s
             delete ctx;
             return fail(nullptr, FUTBOL_EUNSUPPORTED, "total_time too long for the 14-bit step counter");
         }
-        for (const char* f : {"px", "py", "vx", "vy", "bx", "by"}) add(f, 0, (int64_t)Nb * B);
+        for (const char* f : {"pxy", "vxy", "bxy"}) add(f, 0, (int64_t)2 * Nb * B);  // [Nb][B][2]
         add("meta", 1, B);
         add("ep_ret", 0, B);
         add("ckey", 3, (int64_t)P * B);
@@ -294,12 +294,9 @@ extern "C" int futbol_create(const FutbolConfig* cfg, int32_t device, uint64_t s
         if ((he = hipMemcpy(ctx->d_params, &hp, sizeof(hp), hipMemcpyHostToDevice)) != hipSuccess)
             return bail(he, "hipMemcpy(params)");
         V1Ptrs& s = ctx->v1;
-        s.px = (double*)fptr("px");
-        s.py = (double*)fptr("py");
-        s.vx = (double*)fptr("vx");
-        s.vy = (double*)fptr("vy");
-        s.bx = (double*)fptr("bx");
-        s.by = (double*)fptr("by");
+        s.pxy = (double2*)fptr("pxy");
+        s.vxy = (double2*)fptr("vxy");
+        s.bxy = (double2*)fptr("bxy");
         s.meta = (uint64_t*)fptr("meta");
         s.ep_ret = (double*)fptr("ep_ret");
         s.ckey = (uint16_t*)fptr("ckey");

@@ -5,7 +5,9 @@
 // of per-body or per-pair quantities are [k][B].
 //
 // v1 (envs_v1.Futbol, Nb = 2N+1 bodies in the order A0..A(N-1),B0..B(N-1),ball):
-//   px py vx vy bx by : f64 [Nb][B]   cpBody.p, .v, .v_bias
+//   pxy vxy bxy       : f64 [Nb][B][2] cpBody.p, .v, .v_bias as (x, y) pairs: one 16-byte
+//                                    load / store per lane and vector (half the memory
+//                                    instructions of separate x and y arrays)
 //   meta              : u64 [B]       packed scalars, see Meta below
 //   ep_ret            : f64 [B]       running return of the current episode
 //   ckey              : u16 [P][B]    arbiter cache: pair id | age << 12
@@ -16,6 +18,7 @@
 //   view              : f64 [8][B]    frozen Easy_Agent views (ai_1, ai_2, opp_1, opp_2) x (x,y)
 //   meta, ep_ret, score (u32 [2][B]), stat_ret, stat_cnt
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace futbol {
@@ -53,7 +56,7 @@ __host__ __device__ constexpr int v1_nbodies(int N) { return 2 * N + 1; }
 __host__ __device__ constexpr int v1_npairs(int N) { return v1_nbodies(N) * kNSeg + v1_nbodies(N) * (v1_nbodies(N) - 1) / 2; }
 
 struct V1Ptrs {
-    double *px, *py, *vx, *vy, *bx, *by;
+    double2 *pxy, *vxy, *bxy;  // [Nb][B]
     uint64_t* meta;
     double* ep_ret;
     uint16_t* ckey;

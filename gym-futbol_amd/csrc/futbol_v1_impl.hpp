@@ -53,8 +53,10 @@ constexpr double kE = 0.2;  // elasticity of players and ball; segments 0
 #ifndef FUTBOL_CK_SMALL
 #define FUTBOL_CK_SMALL 6
 #endif
+// N >= 6: 2 (register pressure: those instances run at the 512-VGPR limit with spills, where code
+// generation failed the instance matrix test with 8, DESIGN.md section 6 "compiler")
 template <int N>
-constexpr int CKN = N >= 5 ? FUTBOL_CK_LARGE : FUTBOL_CK_SMALL;
+constexpr int CKN = N >= 6 ? 2 : (N >= 5 ? FUTBOL_CK_LARGE : FUTBOL_CK_SMALL);
 // entries beyond CKN read per batch of independent loads (5v5 and up: registers are exhausted)
 template <int N>
 constexpr int CBN = N >= 5 ? 1 : 4;
@@ -65,15 +67,15 @@ constexpr int CBN = N >= 5 ? 1 : 4;
 #ifndef FUTBOL_SPILL_REGS
 #define FUTBOL_SPILL_REGS 4
 #endif
-#ifndef FUTBOL_SPILL_REGS10
-#define FUTBOL_SPILL_REGS10 2
+#ifndef FUTBOL_SPILL_REGS_BIG  // N >= 6 (10v10 measured 2 best in round 2; 0 now, for register pressure)
+#define FUTBOL_SPILL_REGS_BIG 0
 #endif
 #ifndef FUTBOL_SPILL_REGS2
 #define FUTBOL_SPILL_REGS2 0
 #endif
-// (N = 6..9, with 1-3 LDS slots, take the 10v10 count; N = 1, 3, 4 rarely spill: none)
+// (N = 6..10 share one count; N = 1, 3, 4 rarely spill: none)
 template <int N>
-constexpr int KXN = N == 5 ? FUTBOL_SPILL_REGS : (N >= 6 ? FUTBOL_SPILL_REGS10 : (N == 2 ? FUTBOL_SPILL_REGS2 : 0));
+constexpr int KXN = N == 5 ? FUTBOL_SPILL_REGS : (N >= 6 ? FUTBOL_SPILL_REGS_BIG : (N == 2 ? FUTBOL_SPILL_REGS2 : 0));
 
 // Diagnostic build only (-DFUTBOL_STAMPS, bench.py --stamps): per-wave s_memtime at phase
 // boundaries, accumulated into st.stamps[wave][slot] (kStampStride slots per wave: 0-10 phases,
@@ -1327,12 +1329,13 @@ __device__ __forceinline__ void load_bodies(const V1Ptrs& st, int env, int B, En
     sfor<V1Shape<N>::Nb>([&](auto K) {
         constexpr int k = K;
         const size_t o = (size_t)k * B + env;
-        e.px[k] = st.px[o];
-        e.py[k] = st.py[o];
-        e.vx[k] = st.vx[o];
-        e.vy[k] = st.vy[o];
-        e.bx[k] = st.bx[o];
-        e.by[k] = st.by[o];
+        const double2 p = st.pxy[o], v = st.vxy[o], vb = st.bxy[o];
+        e.px[k] = p.x;
+        e.py[k] = p.y;
+        e.vx[k] = v.x;
+        e.vy[k] = v.y;
+        e.bx[k] = vb.x;
+        e.by[k] = vb.y;
     });
 }
 template <int N>
@@ -1348,12 +1351,9 @@ __device__ __forceinline__ void store_env(const V1Ptrs& st, int env, int B, cons
     sfor<V1Shape<N>::Nb>([&](auto K) {
         constexpr int k = K;
         const size_t o = (size_t)k * B + env;
-        st.px[o] = e.px[k];
-        st.py[o] = e.py[k];
-        st.vx[o] = e.vx[k];
-        st.vy[o] = e.vy[k];
-        st.bx[o] = e.bx[k];
-        st.by[o] = e.by[k];
+        st.pxy[o] = make_double2(e.px[k], e.py[k]);
+        st.vxy[o] = make_double2(e.vx[k], e.vy[k]);
+        st.bxy[o] = make_double2(e.bx[k], e.by[k]);
     });
     st.meta[env] = e.meta.w;
 }
@@ -1626,7 +1626,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
     if constexpr (kPassDraws<N>) {
         pd.j0 = rs.j;
         bool anyp = false;
-        sfor<2 * N>([&](auto K) { anyp = anyp | ((key[K] == 4) & touch[K]); });
+        sfor<2 * N>([&](auto K) { anyp = anyp | (bool)((int)(key[K] == 4) & (int)touch[K]); });
         if (__ballot(anyp)) {  // wave-uniform: both blocks for every lane of a wave with a passer
             const Philox4 p0 = rs.block(pd.j0), p1 = rs.block(pd.j0 + 1);
             pd.a0 = p0.x[0];

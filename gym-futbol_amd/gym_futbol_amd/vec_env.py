@@ -22,6 +22,9 @@ from . import _native as nat
 from . import spaces as sp
 
 _DT = {"f8": np.float64, "u8": np.uint64, "u4": np.uint32, "u2": np.uint16, "u1": np.uint8}
+# v1 body state is stored as (x, y) pairs per body and env (csrc/futbol_state.hpp): the state dict
+# keeps the reference-shaped names (cpBody p / v / v_bias components), one [Nb * B] array each
+_PAIR_FIELDS = {"pxy": ("px", "py"), "vxy": ("vx", "vy"), "bxy": ("bx", "by")}
 
 
 def _stream_ptr(device):
@@ -196,16 +199,30 @@ class FutbolVecEnv:
         out = {}
         for name, off, t, cnt in self.ctx.fields:
             dt = np.dtype(_DT[t])
-            out[name] = buf[off:off + dt.itemsize * cnt].view(dt).copy()
+            a = buf[off:off + dt.itemsize * cnt].view(dt)
+            if name in _PAIR_FIELDS:  # (x, y) pairs in HBM: returned as the two [Nb * B] arrays
+                x, y = _PAIR_FIELDS[name]
+                out[x], out[y] = a[0::2].copy(), a[1::2].copy()
+            else:
+                out[name] = a.copy()
         return out
 
     def set_state(self, state):
         buf = np.zeros(self.ctx.state_bytes, dtype=np.uint8)
         for name, off, t, cnt in self.ctx.fields:
             dt = np.dtype(_DT[t])
-            a = np.ascontiguousarray(state[name], dtype=dt).reshape(-1)
-            if a.size != cnt:
-                raise ValueError("field %s: expected %d elements, got %d" % (name, cnt, a.size))
+            if name in _PAIR_FIELDS:
+                x, y = _PAIR_FIELDS[name]
+                ax = np.ascontiguousarray(state[x], dtype=dt).reshape(-1)
+                ay = np.ascontiguousarray(state[y], dtype=dt).reshape(-1)
+                if 2 * ax.size != cnt or 2 * ay.size != cnt:
+                    raise ValueError("fields %s/%s: expected %d elements each, got %d/%d" % (x, y, cnt // 2, ax.size, ay.size))
+                a = np.empty(cnt, dtype=dt)
+                a[0::2], a[1::2] = ax, ay
+            else:
+                a = np.ascontiguousarray(state[name], dtype=dt).reshape(-1)
+                if a.size != cnt:
+                    raise ValueError("field %s: expected %d elements, got %d" % (name, cnt, a.size))
             buf[off:off + dt.itemsize * cnt] = a.view(np.uint8)
         with torch.cuda.device(self.device):
             nat.check(nat.load().futbol_set_state(self.ctx.h, buf.ctypes.data, 1, _stream_ptr(self.device)),

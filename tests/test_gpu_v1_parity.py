@@ -44,7 +44,7 @@ def _compare_state(venv, ora, n, B, tag):
 
 # LDS record slots and register-held spill slots per team size (futbol_v1_impl.hpp V1Shape / KXN)
 LDS_SLOTS = {1: 8, 2: 7, 3: 6, 4: 5, 5: 4, 6: 3, 7: 2, 8: 4, 9: 3, 10: 2}
-REG_SPILL = {1: 0, 2: 0, 3: 0, 4: 0, 5: 4, 6: 2, 7: 2, 8: 2, 9: 2, 10: 2}
+REG_SPILL = {1: 0, 2: 0, 3: 0, 4: 0, 5: 4, 6: 0, 7: 0, 8: 0, 9: 0, 10: 0}
 
 
 @pytest.mark.parametrize("n,B,T", [(2, 1024, 620), (5, 256, 320), (10, 64, 320), (1, 128, 310), (3, 128, 310),
@@ -160,7 +160,7 @@ def test_teacher_forced_crowded_states(n, B):
     ex0, _, _ = v1_dense_cache(venv.get_state(), n, B)
     assert ex0.sum(1).max() > (8 if n >= 5 else 6), "some env must hold more cache entries than are preloaded"
     # contact records per env: past the LDS slots (K = 7 / 4 / 2 for N = 2 / 5 / 10) the solve holds
-    # the first spill records in registers (0 / 4 / 2 of them) and re-reads the rest from the global
+    # the first spill records in registers (0 / 4 / 0 of them) and re-reads the rest from the global
     # spill area in every sweep -- every one of these paths must run
     lds_slots, reg_spill = LDS_SLOTS[n], REG_SPILL[n]
     most = comps = 0
