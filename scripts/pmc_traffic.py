@@ -49,16 +49,23 @@ def main():
     cwrite = per_kernel(os.path.join(a.prof, "calib_write", "run_counter_collection.csv"), "WRITE_SIZE")
     nb = a.calib_bytes
     calib = {
-        "rd_f64_fetch_ratio": find(cfetch, "rd_f64")[0] / nb,
-        "wr_f64_write_ratio": find(cwrite, "wr_f64")[0] / nb,
+        "rd_f64_fetch_ratio": find(cfetch, "rd_f64(")[0] / nb,
+        "wr_f64_write_ratio": find(cwrite, "wr_f64(")[0] / nb,
         "wr_aos20_write_ratio": find(cwrite, "wr_aos20")[0] / (nb // 80 * 80),
         "wr_u8_write_ratio": find(cwrite, "wr_u8")[0] / nb,
     }
+    try:  # 16 B/lane (the envs_v1 body state since round 3: (x, y) pairs)
+        calib["rd_f64x2_fetch_ratio"] = find(cfetch, "rd_f64x2(")[0] / nb
+        calib["wr_f64x2_write_ratio"] = find(cwrite, "wr_f64x2(")[0] / nb
+    except Exception:
+        pass
     key = ("v1_step_kernel<%d," % a.players) if a.kind == "v1" else "v0_step_kernel"
     f, kname, nf = find(fetch, key)
     w, _, nw = find(write, key)
-    rd = f / calib["rd_f64_fetch_ratio"]
-    wr = w / calib["wr_f64_write_ratio"]
+    # the dominant access width: 16 B/lane for the envs_v1 body state, 8 B/lane for v0's rows
+    wide = a.kind == "v1" and "rd_f64x2_fetch_ratio" in calib
+    rd = f / calib["rd_f64x2_fetch_ratio" if wide else "rd_f64_fetch_ratio"]
+    wr = w / calib["wr_f64x2_write_ratio" if wide else "wr_f64_write_ratio"]
     entry = {"kind": a.kind, "players": a.players, "envs": a.envs, "kernel": kname,
              "launches": [nf, nw], "fetch_size_bytes_raw": f, "write_size_bytes_raw": w,
              "calibration": calib, "read_bytes_corrected": rd, "write_bytes_corrected": wr,
