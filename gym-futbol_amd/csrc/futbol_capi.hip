@@ -251,8 +251,8 @@ extern "C" int futbol_create(const FutbolConfig* cfg, int32_t device, uint64_t s
             delete ctx;
             return fail(nullptr, FUTBOL_EUNSUPPORTED, "game_time too long for the 14-bit step counter");
         }
-        add("row", 0, (int64_t)25 * B);
-        add("view", 0, (int64_t)8 * B);
+        add("row2", 0, (int64_t)13 * 2 * B);  // [13][B][2] (futbol_state.hpp)
+        add("view2", 0, (int64_t)4 * 2 * B);  // [4][B][2]
         add("meta", 1, B);
         add("ep_ret", 0, B);
         add("score", 2, (int64_t)2 * B);
@@ -330,8 +330,8 @@ extern "C" int futbol_create(const FutbolConfig* cfg, int32_t device, uint64_t s
         if ((he = hipMemcpy(ctx->d_params, &hp, sizeof(hp), hipMemcpyHostToDevice)) != hipSuccess)
             return bail(he, "hipMemcpy(params)");
         V0Ptrs& s = ctx->v0;
-        s.row = (double*)fptr("row");
-        s.view = (double*)fptr("view");
+        s.row = (double2*)fptr("row2");
+        s.view = (double2*)fptr("view2");
         s.meta = (uint64_t*)fptr("meta");
         s.ep_ret = (double*)fptr("ep_ret");
         s.score = (uint32_t*)fptr("score");

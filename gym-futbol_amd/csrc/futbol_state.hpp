@@ -14,8 +14,9 @@
 //   cjn               : f64 [P][B]    arbiter cache: jnAcc of the pair's contact
 //   stat_ret, stat_cnt: f64/u32 [B]   finished-episode return sum / count
 // v0 (envs.FutbolEnv):
-//   row               : f64 [25][B]   obs rows ai_1, ai_2, opp_1, opp_2, ball x 5
-//   view              : f64 [8][B]    frozen Easy_Agent views (ai_1, ai_2, opp_1, opp_2) x (x,y)
+//   row2              : f64 [13][B][2] obs rows ai_1, ai_2, opp_1, opp_2, ball x 5 = 25 entries,
+//                                     stored as consecutive pairs (one 16-byte access per pair)
+//   view2             : f64 [4][B][2] frozen Easy_Agent views (ai_1, ai_2, opp_1, opp_2) x (x,y)
 //   meta, ep_ret, score (u32 [2][B]), stat_ret, stat_cnt
 #pragma once
 #include <hip/hip_runtime.h>
@@ -69,8 +70,8 @@ struct V1Ptrs {
 };
 
 struct V0Ptrs {
-    double* row;   // [25][B]
-    double* view;  // [8][B]
+    double2* row;   // [13][B]: (row entry 2q, 2q + 1) pairs of the [25] rows (entry 25: pad)
+    double2* view;  // [4][B]: (x, y) of each frozen view
     uint64_t* meta;
     double* ep_ret;
     uint32_t* score;  // [2][B]

@@ -93,7 +93,7 @@ __device__ __forceinline__ double intercept_chance(double d) /* :122-129, d1 = 1
 
 struct Ctx {
     const V0Params* P;
-    double* view;
+    double2* view;
     int env, B;
     Stream* rs;
 };
@@ -405,8 +405,7 @@ __device__ __forceinline__ void rebind(const Ctx& c, Env& e)
         for (int a = 0; a < 4; ++a) {
             e.vw[2 * a] = e.r[a][0];
             e.vw[2 * a + 1] = e.r[a][1];
-            c.view[(size_t)(2 * a) * c.B + c.env] = e.r[a][0];
-            c.view[(size_t)(2 * a + 1) * c.B + c.env] = e.r[a][1];
+            c.view[(size_t)a * c.B + c.env] = make_double2(e.r[a][0], e.r[a][1]);
         }
     }
 }
@@ -425,14 +424,21 @@ __device__ __forceinline__ void write_obs(const Env& e, bool row_valid, OT* o)
 
 __device__ __forceinline__ void load(const V0Ptrs& st, int env, int B, Env& e, Meta& m)
 {
+    // the 25 row entries as 13 pairs (16-byte loads: half the memory instructions)
 #pragma unroll
-    for (int r = 0; r < 5; ++r)
-#pragma unroll
-        for (int f = 0; f < 5; ++f) e.r[r][f] = st.row[(size_t)(r * 5 + f) * B + env];
+    for (int q = 0; q < 13; ++q) {
+        const double2 v = st.row[(size_t)q * B + env];
+        e.r[(2 * q) / 5][(2 * q) % 5] = v.x;
+        if (2 * q + 1 < 25) e.r[(2 * q + 1) / 5][(2 * q + 1) % 5] = v.y;
+    }
     // the views with the rows, in the same batch of loads: read on every step once the views are
     // frozen (after the first goal or reset), and then the only other HBM reads of the step
 #pragma unroll
-    for (int k = 0; k < 8; ++k) e.vw[k] = st.view[(size_t)k * B + env];
+    for (int a = 0; a < 4; ++a) {
+        const double2 v = st.view[(size_t)a * B + env];
+        e.vw[2 * a] = v.x;
+        e.vw[2 * a + 1] = v.y;
+    }
     m.w = st.meta[env];
     e.owner = m.owner();
     e.last_owner = m.last_owner();
@@ -444,9 +450,10 @@ __device__ __forceinline__ void load(const V0Ptrs& st, int env, int B, Env& e, M
 __device__ __forceinline__ void store(const V0Ptrs& st, int env, int B, const Env& e, Meta& m, bool row_valid)
 {
 #pragma unroll
-    for (int r = 0; r < 5; ++r)
-#pragma unroll
-        for (int f = 0; f < 5; ++f) st.row[(size_t)(r * 5 + f) * B + env] = e.r[r][f];
+    for (int q = 0; q < 13; ++q) {
+        const double y = 2 * q + 1 < 25 ? e.r[(2 * q + 1) / 5][(2 * q + 1) % 5] : 0.0;
+        st.row[(size_t)q * B + env] = make_double2(e.r[(2 * q) / 5][(2 * q) % 5], y);
+    }
     m.set_owner(e.owner);
     m.set_last_owner(e.last_owner);
     m.set_bit(kViewsLive, e.views_live);

@@ -25,6 +25,8 @@ _DT = {"f8": np.float64, "u8": np.uint64, "u4": np.uint32, "u2": np.uint16, "u1"
 # v1 body state is stored as (x, y) pairs per body and env (csrc/futbol_state.hpp): the state dict
 # keeps the reference-shaped names (cpBody p / v / v_bias components), one [Nb * B] array each
 _PAIR_FIELDS = {"pxy": ("px", "py"), "vxy": ("vx", "vy"), "bxy": ("bx", "by")}
+# v0 rows / views are stored as consecutive pairs [n/2][B][2]: the state dict holds the [n][B] arrays
+_GROUP_FIELDS = {"row2": ("row", 25), "view2": ("view", 8)}
 
 
 def _stream_ptr(device):
@@ -203,6 +205,10 @@ class FutbolVecEnv:
             if name in _PAIR_FIELDS:  # (x, y) pairs in HBM: returned as the two [Nb * B] arrays
                 x, y = _PAIR_FIELDS[name]
                 out[x], out[y] = a[0::2].copy(), a[1::2].copy()
+            elif name in _GROUP_FIELDS:
+                key, n = _GROUP_FIELDS[name]
+                B = self.num_envs
+                out[key] = a.reshape(-1, B, 2).transpose(0, 2, 1).reshape(-1, B)[:n].reshape(-1).copy()
             else:
                 out[name] = a.copy()
         return out
@@ -219,6 +225,15 @@ class FutbolVecEnv:
                     raise ValueError("fields %s/%s: expected %d elements each, got %d/%d" % (x, y, cnt // 2, ax.size, ay.size))
                 a = np.empty(cnt, dtype=dt)
                 a[0::2], a[1::2] = ax, ay
+            elif name in _GROUP_FIELDS:
+                key, n = _GROUP_FIELDS[name]
+                B = self.num_envs
+                v = np.ascontiguousarray(state[key], dtype=dt).reshape(-1)
+                if v.size != n * B:
+                    raise ValueError("field %s: expected %d elements, got %d" % (key, n * B, v.size))
+                full = np.zeros((cnt // B, B), dtype=dt)
+                full[:n] = v.reshape(n, B)
+                a = full.reshape(-1, 2, B).transpose(0, 2, 1).reshape(-1)
             else:
                 a = np.ascontiguousarray(state[name], dtype=dt).reshape(-1)
                 if a.size != cnt:

@@ -62,8 +62,8 @@ def main():
     key = ("v1_step_kernel<%d," % a.players) if a.kind == "v1" else "v0_step_kernel"
     f, kname, nf = find(fetch, key)
     w, _, nw = find(write, key)
-    # the dominant access width: 16 B/lane for the envs_v1 body state, 8 B/lane for v0's rows
-    wide = a.kind == "v1" and "rd_f64x2_fetch_ratio" in calib
+    # the dominant access width: 16 B/lane (the envs_v1 body pairs, the v0 row pairs)
+    wide = "rd_f64x2_fetch_ratio" in calib  # every state array since round 3 (v1 bodies, v0 rows)
     rd = f / calib["rd_f64x2_fetch_ratio" if wide else "rd_f64_fetch_ratio"]
     wr = w / calib["wr_f64x2_write_ratio" if wide else "wr_f64_write_ratio"]
     entry = {"kind": a.kind, "players": a.players, "envs": a.envs, "kernel": kname,
