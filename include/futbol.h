@@ -131,7 +131,11 @@ int futbol_invalid_actions(FutbolCtx* ctx, uint64_t* out, void* stream);
 
 /* Raw SoA state, for checkpoint/restore and parity tests.  The layout is
    described field by field: name, byte offset, element type code
-   (0 f64, 1 u64, 2 u32, 3 u16, 4 u8), element count. */
+   (0 f64, 1 u64, 2 u32, 3 u16, 4 u8), element count.  Vectors are stored as
+   consecutive pairs (v1 "pxy" / "vxy" / "bxy": [Nb][B][2]; v0 "row2": the 25
+   row entries as [13][B][2], "view2": [4][B][2]); the Python get_state /
+   set_state present them as the reference-shaped px, py, ..., row, view
+   arrays (csrc/futbol_state.hpp). */
 int futbol_state_bytes(const FutbolCtx* ctx, size_t* bytes);
 int futbol_state_field(const FutbolCtx* ctx, int32_t index, const char** name, size_t* offset,
                        int32_t* type_code, int64_t* count);
