@@ -107,51 +107,62 @@ def algo_bytes_per_env_step(kind, n, out_bytes):
 
 
 def cpu_threads():
-    """The host threads this process may use: OMP_NUM_THREADS (16 on the GPU box, its CPU share
-    per GPU) or the affinity mask, at most 16."""
+    """Every host core this process may run on (its affinity mask): SURVEY 8(d) times the restatement
+    "on all host cores"."""
+    if hasattr(os, "sched_getaffinity"):
+        return max(1, len(os.sched_getaffinity(0)))
+    return max(1, os.cpu_count() or 1)
+
+
+def omp_share():
+    """OMP_NUM_THREADS when set (16 on the GPU box: its CPU share per GPU), else None."""
     try:
         t = int(os.environ.get("OMP_NUM_THREADS", "0"))
     except ValueError:
-        t = 0
-    if t <= 0:
-        t = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    return max(1, min(16, t))
+        return None
+    return t if t > 0 else None
 
 
-def cpu_baseline(kind, n, budget_s=10.0, B=65536):
-    """Oracle (faithful build) on a bounded sample of the same workload: envs split over the
-    host's threads with OpenMP (the restatement on all host cores), and 1 thread."""
+def cpu_baseline(kind, n, budget_s=8.0, B=65536):
+    """The oracle (faithful build) on the same B-env workload: every env stepped by the C loop of
+    orc_v1_run / orc_v0_vec_run (synthetic Philox actions, auto-reset, obs / reward written every step,
+    no Python per step), envs split over OpenMP threads -- on all host cores (`value`, `cores`), on
+    the OMP_NUM_THREADS share and on 1 thread.  Each figure is a ~budget_s run whose step count is
+    extrapolated from a calibration run of at least 0.5 s."""
     from oracle import oracle as O
+    if kind == "v1":
+        ora = O.V1Vec(B, N=n, seed=0)
+    else:
+        ora = O.V0Vec(B, seed=0, random_opp=False)
+    ora.reset()
 
     def timed(nthreads):
-        if kind == "v1":
-            ora = O.V1Vec(B, N=n, seed=0)
-            nact, adim = 5, 2 * n
-        else:
-            ora = O.V0Vec(B, seed=0, random_opp=False)
-            nact, adim = 16, 1
-        ora.reset()
-        rng = np.random.default_rng(1234)
-        steps = 0
+        steps = 1
+        while True:  # calibration
+            t0 = time.perf_counter()
+            ora.run(steps, 1234, nthreads)
+            dt = time.perf_counter() - t0
+            if dt >= 0.5 or steps >= 1 << 20:
+                break
+            steps *= 2
+        steps = max(1, int(steps * budget_s / dt))
         t0 = time.perf_counter()
-        while time.perf_counter() - t0 < budget_s:
-            a = rng.integers(0, nact, (B, adim)).astype(np.int32)
-            ora.step(a if kind == "v1" else a.reshape(-1), nthreads=nthreads)
-            steps += 1
+        eps, _ = ora.run(steps, 1234, nthreads)
         dt = time.perf_counter() - t0
-        return steps * B / dt, steps, dt
+        return {"value": steps * B / dt, "threads": nthreads, "steps": steps, "seconds": dt, "episodes": eps}
 
     what = "envs_v1 %dv%d" % (n, n) if kind == "v1" else "v0 hard-coded-opponent"
     T = cpu_threads()
-    v1t, s1, d1 = timed(1)
-    if T > 1:
-        vT, sT, dT = timed(T)
-    else:
-        vT, sT, dT = v1t, s1, d1
-    out = {"value": vT, "unit": "env-steps/s", "cores": T, "kind": "port",
-           "sample": "oracle/liboracle.so (C restatement of the %s step), %d OpenMP threads, %d envs x %d steps "
-                     "(%.1f s); 1 thread: %d steps (%.1f s)" % (what, T, B, sT, dT, s1, d1),
-           "single_thread_value": v1t, "host": host_cpu(), "reference_v0_python": REF_V0_PYTHON}
+    allc = timed(T)
+    share = omp_share()
+    sh = timed(share) if share and share != T else None
+    one = timed(1) if T > 1 else allc
+    out = {"value": allc["value"], "unit": "env-steps/s", "cores": T, "kind": "port",
+           "sample": "oracle/liboracle.so (C restatement of the %s step), %d envs x %d steps (%.1f s) on %d OpenMP "
+                     "threads = every core of the affinity mask; each thread steps its own envs in a C loop "
+                     "(synthetic Philox actions, auto-reset)" % (what, B, allc["steps"], allc["seconds"], T),
+           "all_cores": allc, "omp_share": sh, "single_thread": one, "single_thread_value": one["value"],
+           "host": host_cpu(), "reference_v0_python": REF_V0_PYTHON}
     if kind == "v1" and n == 2:
         out["c1"] = c1_baseline(n)
     return out
@@ -285,6 +296,65 @@ def stamps_report(venv, one_step, args):
     venv.close()
 
 
+def launch_ranks(n, argv):
+    """`--gpus N` (N > 1) without an external launcher: N child processes of this same script, rank r
+    on LOCAL_RANK r (its GPU), rendezvous at 127.0.0.1 on a free port -- what torchrun would set up.
+    It runs right after argument parsing, before this process imports the package or touches the GPU
+    (the parent only starts and waits for its children; it never initialises HIP and never execs).
+    Rank 0's JSON line reaches the caller through the inherited stdout.  Returns 0 when every rank
+    succeeded, else the first failing rank's exit status (the other ranks are then terminated, since
+    they would wait for it at the next collective)."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    alive = set(range(n))
+    while alive:
+        for r in sorted(alive):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            alive.discard(r)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                print("bench.py: rank %d exited with status %d; stopping the other ranks" % (r, c),
+                      file=sys.stderr, flush=True)
+                for q in alive:
+                    procs[q].send_signal(signal.SIGTERM)
+        time.sleep(0.1)
+    return rc
+
+
+def launcher_selftest(fail_rank):
+    """CPU check of the launcher (tests/test_bench_launcher.py): the ranks form a gloo world and
+    all-reduce their rank + 1; rank 0 prints {"ranks": world, "sum": ...}.  No GPU, no package."""
+    import torch.distributed as dist
+    rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
+    if rank == fail_rank:
+        sys.exit(3)
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    t = torch.tensor([float(rank + 1)])
+    local = [int(os.environ.get("LOCAL_RANK", "0"))]
+    if world > 1:
+        dist.all_reduce(t)
+        local = [None] * world
+        dist.all_gather_object(local, int(os.environ.get("LOCAL_RANK", "0")))
+    if rank == 0:
+        print(json.dumps({"ranks": world, "sum": float(t.item()), "master_addr": os.environ.get("MASTER_ADDR"),
+                          "local_ranks": local}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -315,7 +385,15 @@ def main():
                     help="--stamps: save every snapshot's per-wave slots [snapshots, waves, 32] to this .npy")
     ap.add_argument("--stamps", action="store_true",
                     help="diagnostic: load the FUTBOL_STAMPS build and print the per-phase cycle breakdown")
+    ap.add_argument("--launcher-selftest", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--launcher-selftest-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU, started here (nothing has touched the GPU yet); under torchrun the
+        # ranks already exist and WORLD_SIZE is set
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if args.launcher_selftest:
+        return launcher_selftest(args.launcher_selftest_fail_rank)
     if args.kind == "c1":  # 1 env on 1 CPU thread, no GPU
         c1 = c1_baseline(args.players)
         print(json.dumps({"metric": "env-steps/sec, 1 env %dv%d envs_v1 step, 1 CPU thread (C1)"

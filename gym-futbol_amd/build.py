@@ -87,7 +87,8 @@ if VARIANT == "bounds":  # diagnostic: index checks that flag and clamp instead 
 
 
 def _deps():
-    return glob.glob(os.path.join(CSRC, "*.hpp")) + [os.path.join(ROOT, "include", "futbol.h"), __file__]
+    return (glob.glob(os.path.join(CSRC, "*.hpp")) + glob.glob(os.path.join(CSRC, "*.h")) +
+            [os.path.join(ROOT, "include", "futbol.h"), __file__])
 
 
 def _stale(target, sources):
@@ -98,12 +99,22 @@ def _stale(target, sources):
 
 
 def _compile(src, force):
+    """One TU.  Its full command line is stamped next to the object (<obj>.cmd): a build with other
+    flags (the env-var knobs above) recompiles instead of reusing an object built differently."""
     obj = os.path.join(OBJ, os.path.basename(src) + ".o")
-    if force or _stale(obj, [src] + _deps()):
-        cmd = [HIPCC] + CFLAGS + _phi_flags(src) + _sched_flags(src) + _big_flags(src) + ["-c", src, "-o", obj]
+    cmd = [HIPCC] + CFLAGS + _phi_flags(src) + _sched_flags(src) + _big_flags(src) + ["-c", src, "-o", obj]
+    stamp = obj + ".cmd"
+    try:
+        with open(stamp) as f:
+            same = f.read() == "\n".join(cmd)
+    except OSError:
+        same = False
+    if force or not same or _stale(obj, [src] + _deps()):
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("hipcc failed for %s:\n%s\n%s" % (src, " ".join(cmd), r.stderr[-8000:]))
+        with open(stamp, "w") as f:
+            f.write("\n".join(cmd))
     return obj
 
 

@@ -144,12 +144,29 @@ class FutbolVecEnv:
                    torch.empty((K, self.num_envs), dtype=self.dtype, device=self.device),
                    torch.empty((K, self.num_envs), dtype=torch.uint8, device=self.device),
                    torch.empty((K, self.num_envs) + self.obs_shape, dtype=self.dtype, device=self.device))
+        else:
+            self._check_rollout_out(out, K)
         obs, rew, done, term = out
         with torch.cuda.device(self.device):
             nat.check(nat.load().futbol_rollout(self.ctx.h, actions.data_ptr(), K, obs.data_ptr(), rew.data_ptr(),
                                                 done.data_ptr(), term.data_ptr(), _stream_ptr(self.device)),
                       self.ctx.h)
         return out
+
+    def _check_rollout_out(self, out, K):
+        """The kernel writes K full slices into each caller buffer through raw pointers: dtype, shape,
+        device and contiguity must be exactly what it assumes, or it would write past the allocation."""
+        if not isinstance(out, (tuple, list)) or len(out) != 4:
+            raise ValueError("rollout out must be a tuple (obs, reward, done, terminal_obs)")
+        want = (((K, self.num_envs) + tuple(self.obs_shape), self.dtype), ((K, self.num_envs), self.dtype),
+                ((K, self.num_envs), torch.uint8), ((K, self.num_envs) + tuple(self.obs_shape), self.dtype))
+        for name, b, (shape, dt) in zip(("obs", "reward", "done", "terminal_obs"), out, want):
+            if not isinstance(b, torch.Tensor) or b.dtype != dt or tuple(b.shape) != shape \
+                    or not b.is_contiguous() or b.device != self.device:
+                raise ValueError("rollout out[%s] must be a contiguous %s tensor of shape %s on %s, got %s"
+                                 % (name, dt, shape, self.device,
+                                    "%s %s %s contiguous=%s" % (b.dtype, tuple(b.shape), b.device, b.is_contiguous())
+                                    if isinstance(b, torch.Tensor) else type(b).__name__))
 
     def random_actions(self, step, seed=1234, out=None):
         """Synthetic policy (iid uniform actions, Philox tag-1 stream), written on device."""
@@ -262,10 +279,12 @@ class FutbolVecEnv:
         a new context with the same configuration: like the reference's constructor it ends in
         reset(), so call reset() before stepping.  seed=None keeps the current seed."""
         if seed is not None and int(seed) != self.seed_value:
-            cfg = self.ctx.cfg
-            self.ctx.close()
+            # the new context first: if it cannot be created the env keeps its live one.  (A hipGraph
+            # captured before seed() still points at the old context's state and must be re-captured.)
             with torch.cuda.device(self.device):
-                self.ctx = nat.Context(cfg, self.device.index, int(seed), self.env_id_base, self.num_envs)
+                ctx = nat.Context(self.ctx.cfg, self.device.index, int(seed), self.env_id_base, self.num_envs)
+            old, self.ctx = self.ctx, ctx
+            old.close()
             self.seed_value = int(seed)
         return [self.seed_value + i for i in range(self.num_envs)]
 
@@ -341,10 +360,11 @@ class SB3VecEnv(_SB3Base):
     def step_wait(self):
         obs, rew, done, info = self.venv.step(self._actions)
         obs_np = obs.cpu().numpy().astype(self.observation_space.dtype)
-        rew_np = rew.cpu().numpy().astype(np.float32)
+        rew_host = rew.cpu().numpy()  # one device-to-host copy of the rewards
+        rew_np = rew_host.astype(np.float32)
         done_np = done.cpu().numpy()
         infos = [{} for _ in range(self.num_envs)]
-        self._ep_ret += rew.cpu().numpy().astype(np.float64)
+        self._ep_ret += rew_host.astype(np.float64)
         self._ep_len += 1
         if done_np.any():
             term = info["terminal_observation"].cpu().numpy().astype(self.observation_space.dtype)

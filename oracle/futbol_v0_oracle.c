@@ -423,6 +423,34 @@ int orc_v0_step(OrcV0 *e, int32_t a0, int32_t a1, double *obs, double *reward)
     return done;
 }
 
+/* bench.py cpu_baseline (C3): B envs, each stepped nsteps times with synthetic Philox actions
+   (tag 1, one word per step: a in [0, 16) -> (a / 4, a % 4)), auto-reset, envs split over nthreads
+   OpenMP threads that each step their own block through all nsteps.  Returns the finished
+   episodes; *ret_sum = the sum of every step's reward. */
+long long orc_v0_vec_run(OrcV0 *envs, int B, int nsteps, uint64_t act_seed, int nthreads, double *ret_sum)
+{
+    long long eps = 0;
+    double tot = 0.0;
+#pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : 1) reduction(+ : eps, tot)
+    for (int i = 0; i < B; ++i) {
+        OrcV0 *e = &envs[i];
+        double obs[30], r;
+        for (int t = 0; t < nsteps; ++t) {
+            OracleRng g = { act_seed, e->env_id, (uint32_t)t, 0, 1 };
+            int32_t a;
+            oracle_words_choice(&g, 1, 16, &a);
+            const int d = orc_v0_step(e, a / 4, a % 4, obs, &r);
+            tot += r;
+            if (d) {
+                ++eps;
+                orc_v0_reset(e, obs);
+            }
+        }
+    }
+    *ret_sum = tot;
+    return eps;
+}
+
 void orc_v0_vec_step(OrcV0 *envs, int B, const int32_t *actions, double *obs, double *reward,
                      uint8_t *done, double *terminal_obs, int nthreads)
 {

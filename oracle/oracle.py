@@ -27,7 +27,7 @@ class OrcV1(C.Structure):
                 ("stamp", C.c_uint32), ("curr_dt", C.c_double),
                 ("arb_exists", C.c_int32 * MAXP), ("arb_stamp", C.c_uint32 * MAXP),
                 ("arb_state", C.c_int32 * MAXP), ("arb_inlist", C.c_int32 * MAXP),
-                ("arb_jn", C.c_double * MAXP)]
+                ("arb_jn", C.c_double * MAXP), ("n_out", C.c_uint32), ("n_goal", C.c_uint32)]
 
 
 class OrcV0(C.Structure):
@@ -49,9 +49,11 @@ def lib(portable=False):
     name = "liboracle_portable.so" if portable else "liboracle.so"
     if name in _libs:
         return _libs[name]
-    path = os.path.join(HERE, "_build", name)
+    # FUTBOL_ORACLE_SANITIZE=1: the ASan + UBSan builds of `make sanitize` (tests/conftest.py)
+    san = os.environ.get("FUTBOL_ORACLE_SANITIZE") == "1"
+    path = os.path.join(HERE, "_build", "san" if san else "", name)
     if not os.path.exists(path):
-        subprocess.check_call(["make", "-s", "-C", HERE])
+        subprocess.check_call(["make", "-s", "-C", HERE] + (["sanitize"] if san else []))
     L = C.CDLL(path)
     dp = np.ctypeslib.ndpointer(np.float64, flags="C")
     ip = np.ctypeslib.ndpointer(np.int32, flags="C")
@@ -65,12 +67,17 @@ def lib(portable=False):
     L.orc_v1_vec_step.argtypes = [C.c_void_p, C.c_int, ip, dp, dp, up, C.c_void_p, C.c_int]
     L.orc_v1_run.argtypes = [C.c_void_p, C.c_int, C.c_uint64, C.POINTER(C.c_double)]
     L.orc_v1_run.restype = C.c_int
+    L.orc_v1_vec_run.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_uint64, C.c_int, C.POINTER(C.c_double)]
+    L.orc_v1_vec_run.restype = C.c_longlong
+    L.orc_v0_vec_run.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_uint64, C.c_int, C.POINTER(C.c_double)]
+    L.orc_v0_vec_run.restype = C.c_longlong
     L.orc_libm_check.argtypes = [C.c_int64, C.c_double, C.c_double, C.c_uint64] + [C.POINTER(C.c_int64)] * 3
     L.orc_v0_init.argtypes = [C.c_void_p] + [C.c_double] * 6 + [C.c_int] * 3 + [C.c_uint64, C.c_uint32]
     L.orc_v0_reset.argtypes = [C.c_void_p, C.c_void_p]
     L.orc_v0_step.argtypes = [C.c_void_p, C.c_int32, C.c_int32, dp, C.POINTER(C.c_double)]
     L.orc_v0_step.restype = C.c_int
     L.orc_v0_vec_step.argtypes = [C.c_void_p, C.c_int, ip, dp, dp, up, C.c_void_p, C.c_int]
+    L.orc_v1_set_sq_mask.argtypes = [C.c_int]
     L.orc_philox.argtypes = [C.POINTER(C.c_uint32)] * 3
     L.orc_draw_u01.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                C.POINTER(C.c_double), C.POINTER(C.c_double)]
@@ -109,6 +116,13 @@ class V1Vec:
         self.L.orc_v1_vec_step(C.byref(self.envs), self.B, actions, obs, rew, done, term.ctypes.data, nthreads)
         return obs, rew, done.astype(bool), term
 
+    def run(self, nsteps, act_seed=1234, nthreads=1):
+        """nsteps steps of every env in one C call (synthetic Philox actions, auto-reset), envs split
+        over nthreads threads; returns (finished episodes, their return sum)."""
+        ret = C.c_double()
+        eps = self.L.orc_v1_vec_run(C.byref(self.envs), self.B, int(nsteps), act_seed, int(nthreads), C.byref(ret))
+        return eps, ret.value
+
 
 class V0Vec:
     """B independent v0 FutbolEnv envs with DummyVecEnv semantics."""
@@ -139,6 +153,13 @@ class V0Vec:
         self.L.orc_v0_vec_step(C.byref(self.envs), self.B, actions, obs.reshape(-1), rew, done,
                                term.ctypes.data, nthreads)
         return obs, rew, done.astype(bool), term
+
+    def run(self, nsteps, act_seed=1234, nthreads=1):
+        """nsteps steps of every env in one C call (synthetic Philox actions, auto-reset), envs split
+        over nthreads threads; returns (finished episodes, the sum of every step's reward)."""
+        ret = C.c_double()
+        eps = self.L.orc_v0_vec_run(C.byref(self.envs), self.B, int(nsteps), act_seed, int(nthreads), C.byref(ret))
+        return eps, ret.value
 
 
 def philox(ctr, key, portable=False):

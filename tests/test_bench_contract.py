@@ -29,27 +29,51 @@ def test_committed_traffic_entry(n):
     assert algo <= traffic < 1.5 * algo
 
 
-def test_cpu_threads_bounds(monkeypatch):
-    monkeypatch.setenv("OMP_NUM_THREADS", "64")
-    assert bench.cpu_threads() == 16
+def test_cpu_threads_all_host_cores(monkeypatch):
+    # the restatement on ALL host cores -- the affinity mask, whatever OMP_NUM_THREADS says
     monkeypatch.setenv("OMP_NUM_THREADS", "3")
-    assert bench.cpu_threads() == 3
+    assert bench.cpu_threads() == len(os.sched_getaffinity(0))
+    assert bench.omp_share() == 3
     monkeypatch.delenv("OMP_NUM_THREADS")
-    assert 1 <= bench.cpu_threads() <= 16
+    assert bench.omp_share() is None
 
 
 @pytest.mark.parametrize("kind", ["v1", "v0"])
 def test_cpu_baseline_record(kind, monkeypatch):
     monkeypatch.setenv("OMP_NUM_THREADS", "2")
     r = bench.cpu_baseline(kind, 2, budget_s=0.2, B=256)
-    assert r["unit"] == "env-steps/s" and r["kind"] == "port" and r["cores"] == 2
-    assert r["value"] > 0 and r["single_thread_value"] > 0
-    assert "2 OpenMP threads" in r["sample"] and "1 thread" in r["sample"]
+    T = len(os.sched_getaffinity(0))
+    assert r["unit"] == "env-steps/s" and r["kind"] == "port" and r["cores"] == T
+    assert r["all_cores"]["threads"] == T and r["value"] == r["all_cores"]["value"] > 0
+    assert r["single_thread"]["threads"] == 1 and r["single_thread_value"] > 0
+    if T != 2:
+        assert r["omp_share"]["threads"] == 2 and r["omp_share"]["value"] > 0
+    assert "%d OpenMP threads" % T in r["sample"]
     assert r["host"]["nproc"] >= 1 and "reference_v0_python" in r
     if kind == "v1":
         c1 = r["c1"]  # 1 env, 1 thread, 100 000 steps
         assert c1["envs"] == 1 and c1["cores"] == 1 and c1["steps"] == 100000 and c1["value"] > 0
         assert c1["episodes"] == 100000 // 300  # fixed 300-step episodes
+
+
+def test_vec_run_matches_single_env_runs():
+    # the all-core loop is orc_v1_run per env: same episodes and returns whatever the thread count
+    from oracle import oracle as O
+    import ctypes as C
+    a = O.V1Vec(16, N=2, seed=3)
+    a.reset()
+    eps_a, ret_a = a.run(650, 1234, 4)
+    L = O.lib()
+    eps_b, ret_b = 0, 0.0
+    for i in range(16):
+        e = O.OrcV1()
+        L.orc_v1_init(C.byref(e), 2, 105.0, 68.0, 30.0, 3, i)
+        import numpy as np
+        L.orc_v1_reset(C.byref(e), np.zeros(20).ctypes.data)
+        r = C.c_double()
+        eps_b += L.orc_v1_run(C.byref(e), 650, 1234, C.byref(r))
+        ret_b += r.value
+    assert eps_a == eps_b == 16 * 2 and abs(ret_a - ret_b) <= 1e-9 * max(1.0, abs(ret_b))
 
 
 def test_metric_labels_per_config():
