@@ -26,6 +26,14 @@ ARCH = os.environ.get("FUTBOL_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fPIC",
           "-Wall", "-Wno-unused-function", "-I" + os.path.join(ROOT, "include")]
+# No pre-RA exec-mask optimization (SIOptimizeExecMaskingPreRA).  With it, the register allocator's
+# live-range-split copies (v_accvgpr_write aN, vM ...) of values live in every lane ended up at the
+# top of a join block BEFORE its exec restore -- executed with the inner branch's lanes only, or none
+# -- in the step instances at high register pressure: the cause of round 3's wrong results and
+# illegal address ("compiler").  scripts/isa_exec_check.py / tests/test_isa_exec.py
+# check every built kernel for the pattern.  FUTBOL_EXEC_OPT_PRE_RA=1 restores LLVM's default.
+if os.environ.get("FUTBOL_EXEC_OPT_PRE_RA", "0") != "1":
+    CFLAGS += ["-mllvm", "-amdgpu-opt-exec-mask-pre-ra=false"]
 # SimplifyCFG folds an if/else whose arms cost up to this many instructions into selects: the
 # default (4) leaves the fp64 arms of the action / contact code as divergent branches (~40 cycles
 # each on a wave64); 20 measured best for the 2v2 step (-1.5% step time).  Only for the N <= 3
@@ -71,6 +79,19 @@ def _big_flags(src):
     return BIG_FLAGS if os.path.basename(src) in BIG_SOURCES else []
 
 
+# diagnostic variants: extra flags for single TUs, FUTBOL_TU_FLAGS="<tu.hip>:<flags>;<tu.hip>:<flags>"
+# (e.g. the round-3 failing configurations, scripts/gpu_fault_r04.sh)
+TU_FLAGS = {}
+for _ent in os.environ.get("FUTBOL_TU_FLAGS", "").split(";"):
+    if ":" in _ent:
+        _tu, _fl = _ent.split(":", 1)
+        TU_FLAGS[_tu.strip()] = _fl.split()
+
+
+def _tu_flags(src):
+    return TU_FLAGS.get(os.path.basename(src), [])
+
+
 def _sched_flags(src):
     b = os.path.basename(src)
     if not SCHED or b not in SCHED_SOURCES:
@@ -98,24 +119,56 @@ def _stale(target, sources):
     return any(os.path.getmtime(s) > t for s in sources)
 
 
+# Code-generation gate ("compiler"): after compiling a TU, its code object is
+# scanned for register copies placed before a join block's exec restore (scripts/isa_exec_check.py),
+# the pattern behind round 3's wrong-result / illegal-address instances.  A TU with a finding is
+# recompiled with the next of these register-allocation / scheduling variants (each changes where the
+# allocator splits live ranges) until none is found; the build fails if every variant has findings.
+# The variant used is recorded in the object's stamp.  FUTBOL_ISA_GATE=0 skips the gate.
+GATE_VARIANTS = [[], ["-mllvm", "-split-spill-mode=size"], ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+                 ["-mllvm", "-split-spill-mode=size", "-mllvm", "-amdgpu-sched-strategy=max-ilp"]]
+GATE = os.environ.get("FUTBOL_ISA_GATE", "1") != "0"
+
+
+def _isa_findings(obj):
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import isa_exec_check
+    return isa_exec_check.check_object(obj)
+
+
 def _compile(src, force):
     """One TU.  Its full command line is stamped next to the object (<obj>.cmd): a build with other
     flags (the env-var knobs above) recompiles instead of reusing an object built differently."""
     obj = os.path.join(OBJ, os.path.basename(src) + ".o")
-    cmd = [HIPCC] + CFLAGS + _phi_flags(src) + _sched_flags(src) + _big_flags(src) + ["-c", src, "-o", obj]
+    base = [HIPCC] + CFLAGS + _phi_flags(src) + _sched_flags(src) + _big_flags(src) + _tu_flags(src)
     stamp = obj + ".cmd"
     try:
         with open(stamp) as f:
-            same = f.read() == "\n".join(cmd)
+            same = f.read().split("\n#gate")[0] == "\n".join(base)
     except OSError:
         same = False
-    if force or not same or _stale(obj, [src] + _deps()):
+    if not (force or not same or _stale(obj, [src] + _deps())):
+        return obj
+    log = []
+    for k, extra in enumerate(GATE_VARIANTS if GATE else [[]]):
+        cmd = base + extra + ["-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("hipcc failed for %s:\n%s\n%s" % (src, " ".join(cmd), r.stderr[-8000:]))
-        with open(stamp, "w") as f:
-            f.write("\n".join(cmd))
-    return obj
+        found = _isa_findings(obj) if GATE else []
+        log.append("%s: %d finding(s)%s" % (" ".join(extra) or "default", len(found),
+                                            "".join("\n#   %s @ %s: %s" % (f[0][:60], f[1], "; ".join(f[2][:3]))
+                                                    for f in found[:4])))
+        if not found:
+            with open(stamp, "w") as f:
+                f.write("\n".join(base) + "\n#gate variant %d: %s\n#" % (k, " ".join(extra) or "default") +
+                        "\n#".join(log))
+            if k:
+                print("isa gate: %s built with %s" % (os.path.basename(src), " ".join(extra)), flush=True)
+            return obj
+    os.remove(obj)
+    raise RuntimeError("isa gate: every variant of %s has register copies before an exec restore:\n%s"
+                       % (src, "\n".join(log)))
 
 
 def build(force=False, jobs=None, verbose=True):

@@ -350,19 +350,29 @@ extern "C" int futbol_create(const FutbolConfig* cfg, int32_t device, uint64_t s
 extern "C" int futbol_destroy(FutbolCtx* ctx)
 {
     if (!ctx) return FUTBOL_OK;
-    hipSetDevice(ctx->device);
-    if (ctx->d_state) hipFree(ctx->d_state);
-    if (ctx->d_spill) hipFree(ctx->d_spill);
-    if (ctx->d_params) hipFree(ctx->d_params);
-    if (ctx->d_invalid) hipFree(ctx->d_invalid);
+    // every resource is released whatever fails; the first failure is reported (the context is gone
+    // afterwards, so its text goes to the global error string)
+    hipError_t first = hipSuccess;
+    auto keep = [&](hipError_t e) {
+        if (first == hipSuccess && e != hipSuccess) first = e;
+    };
+    keep(hipSetDevice(ctx->device));
+    if (ctx->d_state) keep(hipFree(ctx->d_state));
+    if (ctx->d_spill) keep(hipFree(ctx->d_spill));
+    if (ctx->d_params) keep(hipFree(ctx->d_params));
+    if (ctx->d_invalid) keep(hipFree(ctx->d_invalid));
 #ifdef FUTBOL_CRUMBS
-    if (ctx->d_stamps) hipHostFree(ctx->d_stamps);
+    if (ctx->d_stamps) keep(hipHostFree(ctx->d_stamps));
 #else
-    if (ctx->d_stamps) hipFree(ctx->d_stamps);
+    if (ctx->d_stamps) keep(hipFree(ctx->d_stamps));
 #endif
     for (auto e : ctx->t_ev)
-        if (e) hipEventDestroy(e);
+        if (e) keep(hipEventDestroy(e));
     delete ctx;
+    if (first != hipSuccess) {
+        g_create_error = std::string("futbol_destroy: ") + hipGetErrorString(first);
+        return FUTBOL_EHIP;
+    }
     return FUTBOL_OK;
 }
 

@@ -291,8 +291,9 @@ __host__ __device__ inline double glibc_cos(double x, const double* tab = kSinCo
 // computation only where |x^2 - midpoint| < 2^-6 ulp (exact test: lo = fma(x, x, -x*x) is the
 // exact rounding error of x*x).  Main path only: x normal with x^2 in [2^-738, 2^738], x*x
 // elsewhere (never reached by squared coordinate differences).  Tables: futbol_powtab.h.
-static constexpr double kPowLog[128 * 3] = {FUTBOL_POW_LOG_ROWS};
-static constexpr uint64_t kPowExp[256] = {FUTBOL_POW_EXP_ROWS};
+alignas(16) static constexpr double kPowLog[128 * 3] = {FUTBOL_POW_LOG_ROWS};
+alignas(16) static constexpr uint64_t kPowExp[256] = {FUTBOL_POW_EXP_ROWS};
+constexpr int kPowTabBytes = (int)(sizeof(kPowLog) + sizeof(kPowExp));  // 5 KB
 
 __host__ __device__ inline double bits_to_f64(uint64_t u)
 {
@@ -419,6 +420,97 @@ __host__ __device__ __forceinline__ void glibc_pow2_batch(const double (&x)[M], 
 #pragma unroll
         for (int i = 0; i < M; ++i) h[i] = bit == (1u << i) ? f : h[i];
         pend &= pend - 1u;
+    }
+}
+
+// Copy the pow tables (kPowLog, then kPowExp: 5 KB) into `lds` with every lane of a one-wave block,
+// 16 bytes per lane and access (lanes 0..63: 5 loads, no dependence between them); returns the LDS
+// copies' addresses.  The caller has the wave converged, and `lds` 16-byte aligned and not in use.
+__device__ __forceinline__ void stage_pow_tables(void* lds, const double*& logt, const uint64_t*& expt)
+{
+    const uint4* sl = reinterpret_cast<const uint4*>(kPowLog);
+    const uint4* se = reinterpret_cast<const uint4*>(kPowExp);
+    uint4* d = reinterpret_cast<uint4*>(lds);
+    constexpr int NL = (int)sizeof(kPowLog) / 16, NE = (int)sizeof(kPowExp) / 16;  // 192, 128
+    const int l = (int)(threadIdx.x & 63u);
+    const uint4 a0 = sl[l], a1 = sl[l + 64], a2 = sl[l + 128], b0 = se[l], b1 = se[l + 64];
+    d[l] = a0;
+    d[l + 64] = a1;
+    d[l + 128] = a2;
+    d[NL + l] = b0;
+    d[NL + l + 64] = b1;
+    static_assert(NL == 192 && NE == 128, "5 uint4 per lane");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    logt = reinterpret_cast<const double*>(lds);
+    expt = reinterpret_cast<const uint64_t*>(d + NL);
+}
+
+// glibc_pow2_need (below) with the tables staged in LDS (stage_pow_tables into `lds`) when some lane
+// of the wave needs glibc's path: two LDS lookups per slow round instead of two global ones
+template <int M>
+__device__ __forceinline__ void glibc_pow2_need_lds(const double (&x)[M], double (&h)[M], uint64_t need, void* lds);
+
+// h[i] = glibc pow(x[i], 2.0) for the squares whose bit i of `need` is set, x*x for the others
+// (squares whose value cannot matter for this lane: the caller's superset of the used ones).  Like
+// glibc_pow2_batch, the near-midpoint squares are recomputed one per lane per round, so a wave runs
+// max-over-lanes(pending) rounds; up to 64 squares.
+template <int M>
+__host__ __device__ __forceinline__ void glibc_pow2_need(const double (&x)[M], double (&h)[M], uint64_t need,
+                                                        const double* logt = kPowLog, const uint64_t* expt = kPowExp)
+{
+    static_assert(M <= 64, "pending mask");
+    uint64_t pend = 0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+        h[i] = x[i] * x[i];
+        pend |= (uint64_t)pow2_near_midpoint(h[i], fma(x[i], x[i], -h[i])) << i;
+    }
+    pend &= need;
+#ifdef FUTBOL_DIAG_PLAIN_SQ  // diagnostic builds only (cost of the exact squares): x*x, NOT glibc's
+    pend = 0u;
+#endif
+    while (__builtin_expect(pend != 0u, 0)) {
+        const uint64_t bit = pend & (0ull - pend);
+        double v = 0.0;
+#pragma unroll
+        for (int i = 0; i < M; ++i) v = bit == (1ull << i) ? x[i] : v;
+        const double f = glibc_pow2_full(v, logt, expt);
+#pragma unroll
+        for (int i = 0; i < M; ++i) h[i] = bit == (1ull << i) ? f : h[i];
+        pend &= pend - 1u;
+    }
+}
+
+template <int M>
+__device__ __forceinline__ void glibc_pow2_need_lds(const double (&x)[M], double (&h)[M], uint64_t need, void* lds)
+{
+    static_assert(M <= 64, "pending mask");
+    uint64_t pend = 0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+        h[i] = x[i] * x[i];
+        pend |= (uint64_t)pow2_near_midpoint(h[i], fma(x[i], x[i], -h[i])) << i;
+    }
+    pend &= need;
+#ifdef FUTBOL_DIAG_PLAIN_SQ  // diagnostic builds only (cost of the exact squares): x*x, NOT glibc's
+    pend = 0u;
+#endif
+    if (__builtin_expect(__ballot(pend != 0u) != 0ull, 0)) {  // wave-uniform
+        const double* logt;
+        const uint64_t* expt;
+        stage_pow_tables(lds, logt, expt);
+        while (pend != 0u) {
+            const uint64_t bit = pend & (0ull - pend);
+            double v = 0.0;
+#pragma unroll
+            for (int i = 0; i < M; ++i) v = bit == (1ull << i) ? x[i] : v;
+            const double f = glibc_pow2_full(v, logt, expt);
+#pragma unroll
+            for (int i = 0; i < M; ++i) h[i] = bit == (1ull << i) ? f : h[i];
+            pend &= pend - 1u;
+        }
     }
 }
 

@@ -499,7 +499,6 @@ __device__ __forceinline__ void v0_step_body(const V0Params* __restrict__ P, con
         a0 = a0 > 3 ? 3 : a0;
         a1 = a1 > 3 ? 3 : a1;
     }
-    if (bad) atomicAdd(st.invalid, (unsigned long long)bad);
 
     double ob[5], oa1[5], oa2[5], oown[5];
     const int oidx = e.owner <= 3 ? (int)e.owner : 4;
@@ -617,6 +616,10 @@ __device__ __forceinline__ void v0_step_body(const V0Params* __restrict__ P, con
     reward[env] = (OT)rw;
     done_out[env] = done ? 1 : 0;
     store(st, env, B, e, m, row_valid);
+    // the clamped-action count at the very end, where no value is live across the atomic's divergent
+    // `if` (see futbol_v1_impl.hpp: a copy the register allocator placed at the join of that `if`
+    // before its exec restore miscompiled the large envs_v1 instances)
+    if (bad) atomicAdd(st.invalid, (unsigned long long)bad);
 }
 
 // ROLL (nsteps > 1): open-loop rollout (futbol_rollout), step k on the k-th [B][...] slice of every

@@ -32,6 +32,7 @@
 #include <stdint.h>
 #include <type_traits>
 #include "futbol_kernels.hpp"
+#include "futbol_math.hpp"
 #include "futbol_v1_params.hpp"
 #include "futbol_rng.hpp"
 #include "futbol_state.hpp"
@@ -55,8 +56,11 @@ constexpr double kE = 0.2;  // elasticity of players and ball; segments 0
 #endif
 // N >= 6: 2 (register pressure: those instances run at the 512-VGPR limit with spills, where code
 // generation failed the instance matrix test with 8, DESIGN.md section 6 "compiler")
+#ifndef FUTBOL_CK_BIG
+#define FUTBOL_CK_BIG 2
+#endif
 template <int N>
-constexpr int CKN = N >= 6 ? 2 : (N >= 5 ? FUTBOL_CK_LARGE : FUTBOL_CK_SMALL);
+constexpr int CKN = N >= 6 ? FUTBOL_CK_BIG : (N >= 5 ? FUTBOL_CK_LARGE : FUTBOL_CK_SMALL);
 // entries beyond CKN read per batch of independent loads (5v5 and up: registers are exhausted)
 template <int N>
 constexpr int CBN = N >= 5 ? 1 : 4;
@@ -872,15 +876,31 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
         }
     }
 
-    // cpBodyUpdateVelocity + the reference's limit_velocity callback:
-    // sqrt(vx^2+vy^2) > vmax  <=>  vx^2+vy^2 > T (T = largest double whose rounded sqrt is <= vmax)
+    // cpBodyUpdateVelocity + the reference's limit_velocity callback (ball.py:49-56, player.py:45-52):
+    // l = Vec2d.length = sqrt(vx**2 + vy**2) with Python's `**2` = glibc pow(x, 2), and
+    // l > vmax  <=>  s2 > T (T = largest double whose rounded sqrt is <= vmax).  x*x decides every
+    // body whose s2 is clearly below T; the exact squares are computed (glibc_pow2_need: only the
+    // near-midpoint ones take glibc's path) for the bodies that may clamp, whose scale uses them
+    double vq[2 * S::Nb], vsq[2 * S::Nb];
+    uint64_t vneed = 0;
     sfor<S::Nb>([&](auto K) {
         constexpr int k = K;
         e.vx[k] = e.vx[k] * damping + 0.0 * dt;
         e.vy[k] = e.vy[k] * damping + 0.0 * dt;
-        const double s2 = e.vx[k] * e.vx[k] + e.vy[k] * e.vy[k];
+        vq[2 * k] = e.vx[k];
+        vq[2 * k + 1] = e.vy[k];
         const double thr = k == S::BALL ? P.clamp2_ball : P.clamp2_player;
-        if (s2 > thr) {
+        // |pow - x*x| <= 1 ulp per square: below T (1 - 2^-40) neither s2 exceeds T
+        vneed |= (uint64_t)(e.vx[k] * e.vx[k] + e.vy[k] * e.vy[k] > thr * (1.0 - 0x1.0p-40)) * (3ull << (2 * k));
+    });
+    // (the LDS rows are free here: the narrowphase's staging is consumed, the solve's not yet written)
+    static_assert(sizeof(L.sh->rows) >= (size_t)kPowTabBytes, "pow tables fit the solver rows");
+    glibc_pow2_need_lds<2 * S::Nb>(vq, vsq, vneed, &L.sh->rows[0][0]);
+    sfor<S::Nb>([&](auto K) {
+        constexpr int k = K;
+        const double s2 = vsq[2 * k] + vsq[2 * k + 1];
+        const double thr = k == S::BALL ? P.clamp2_ball : P.clamp2_player;
+        if (((vneed >> (2 * k)) & 1u) && s2 > thr) {
             constexpr double vmax = k == S::BALL ? kBallVmax : kPlayerVmax;
             const double sc = vmax / sqrt(s2);
             e.vx[k] = e.vx[k] * sc;
@@ -1448,12 +1468,15 @@ struct PassDraws {
 };
 
 template <int N, int side, int me>
-__device__ __forceinline__ void pass_target(const Env<N>& e, Stream& rs, PassDraws& pd, int ar, double& tx, double& ty)
+__device__ __forceinline__ void pass_target(const Env<N>& e, Stream& rs, PassDraws& pd, int ar, double& tx, double& ty,
+                                            const double (&sq)[4 * N + 3], double& sx, double& sy)
 {
     constexpr int base = side * N;
     if constexpr (N == 1) {
         tx = e.px[base];
         ty = e.py[base];
+        sx = sq[2 * base];
+        sy = sq[2 * base + 1];
         return;
     } else {
         // random.choices over teammates != self.  With one teammate (N = 2) every choice of this
@@ -1498,11 +1521,15 @@ __device__ __forceinline__ void pass_target(const Env<N>& e, Stream& rs, PassDra
         // 1 * px, the others +-0), so LLVM cannot turn it into a scratch-memory lookup table
         tx = 0.0;
         ty = 0.0;
+        sx = 0.0;
+        sy = 0.0;
         sfor<N>([&](auto Q) {
             constexpr int q = Q;
             const double sel = q == t ? 1.0 : 0.0;
             tx = __builtin_fma(sel, e.px[base + q], tx);
             ty = __builtin_fma(sel, e.py[base + q], ty);
+            sx = __builtin_fma(sel, sq[2 * (base + q)], sx);  // the target's squares (ball - teammate)^2
+            sy = __builtin_fma(sel, sq[2 * (base + q) + 1], sy);
         });
     }
 }
@@ -1596,7 +1623,9 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
             if constexpr (i & 1) key[N + (i >> 1)] = a; else arrow[N + (i >> 1)] = a;
         });
     }
+#ifdef FUTBOL_DIAG_EARLY_ATOMIC  // diagnostic builds only: the round-3 position of the count (see below)
     if (bad && live) atomicAdd(st.invalid, (unsigned long long)bad);
+#endif
     FUTBOL_STAMP(1);
 
     // _ball_to_team_distance_arr(team_A), ball_init (:433-435)
@@ -1635,6 +1664,38 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
             pd.b1 = p1.x[1];
         }
     }
+    // get_vec's magnitude (envs_v1/futbol_env.py:56-59), np.sqrt(vec[0]**2 + vec[1]**2) with glibc
+    // pow squares: the direction S * d / |d| feeds the state (round 3 squared with x*x here, and one
+    // 5v5 env in 8 192 flipped an outcome within 600 steps: tests/test_oracle_modes.py).  Positions
+    // do not change in the loop, so every candidate d is known now -- ball - player k (press; a
+    // pass to teammate k squares k - ball, the same squares) and goal - ball (shoot) -- and their
+    // exact squares are one batch: the near-midpoint ones of the squares some lane may use
+    constexpr int NSQ = 4 * N + 3;
+    double sqin[NSQ], sq[NSQ];
+    uint64_t sqneed = 0;
+    {
+        uint32_t pass_side = 0, shoot_side = 0;
+        sfor<2 * N>([&](auto K) {
+            constexpr int k = K;
+            constexpr int side = k < N ? 0 : 1;
+            pass_side |= (uint32_t)((key[k] == 4) & touch[k]) << side;
+            shoot_side |= (uint32_t)((key[k] == 2) & touch[k]) << side;
+        });
+        sfor<2 * N>([&](auto K) {
+            constexpr int k = K;
+            constexpr int side = k < N ? 0 : 1;
+            sqin[2 * k] = e.px[BL] - e.px[k];
+            sqin[2 * k + 1] = e.py[BL] - e.py[k];
+            const bool press = (key[k] == 3) & !touch[k] & (arrow[k] == 0);
+            sqneed |= (uint64_t)(press | (bool)((pass_side >> side) & 1u)) * (3ull << (2 * k));
+        });
+        sqin[4 * N] = W - e.px[BL];      // shoot of side 0 (goal at x = W)
+        sqin[4 * N + 1] = 0.0 - e.px[BL];  // side 1 (goal at x = 0)
+        sqin[4 * N + 2] = H / 2 - e.py[BL];
+        sqneed |= ((uint64_t)(shoot_side & 1u) << (4 * N)) | ((uint64_t)(shoot_side >> 1) << (4 * N + 1)) |
+                  ((uint64_t)(shoot_side != 0) << (4 * N + 2));
+    }
+    glibc_pow2_need_lds<NSQ>(sqin, sq, sqneed, &sh.rows[0][0]);  // (rows: unused until space_step)
     sfor<2 * N>([&](auto K) {
         constexpr int k = K;
         constexpr int side = k < N ? 0 : 1;
@@ -1646,7 +1707,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
         const bool shoot = (ky == 2) & tk;              // (:344-368)
         const bool press = (ky == 3) & !tk & (ar == 0); // (:371-391)
         const bool pass = (ky == 4) & tk;               // (:394-419)
-        double tx = 0.0, ty = 0.0;
+        double tx = 0.0, ty = 0.0, tsx = 0.0, tsy = 0.0;
         if constexpr (N == 2) {
             // one teammate: get_pass_target_teammate always returns it (team.py:136-180); its
             // draws are one-item choices (floor(u * 1) = 0) that only advance the stream: one,
@@ -1656,20 +1717,24 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
             const bool way = ((ar == 1) & (my > 0)) | ((ar == 2) & (mx > 0)) | ((ar == 3) & (my < 0)) | ((ar == 4) & (mx < 0));
             tx = e.px[mate];
             ty = e.py[mate];
+            tsx = sq[2 * mate];
+            tsy = sq[2 * mate + 1];
             rs.skip(pass ? (way ? 2u : 1u) : 0u);
         } else {
 #ifdef FUTBOL_DIAG_NOPASS  // diagnostic only (wrong results): the cost of the pass-target draws
             tx = e.px[side * N];
             ty = e.py[side * N];
 #else
-            if (pass) pass_target<N, side, k - side * N>(e, rs, pd, ar, tx, ty);
+            if (pass) pass_target<N, side, k - side * N>(e, rs, pd, ar, tx, ty, sq, tsx, tsy);
 #endif
         }
         const double gx = side == 0 ? W : 0.0, gy = H / 2;
         const double ox = press ? e.px[k] : e.px[BL], oy = press ? e.py[k] : e.py[BL];
         const double qx = press ? e.px[BL] : (shoot ? gx : tx), qy = press ? e.py[BL] : (shoot ? gy : ty);
         const double dx = qx - ox, dy = qy - oy;
-        const double mag = sqrt(dx * dx + dy * dy);
+        const double sx = press ? sq[2 * k] : (shoot ? sq[4 * N + side] : tsx);
+        const double sy = press ? sq[2 * k + 1] : (shoot ? sq[4 * N + 2] : tsy);
+        const double mag = sqrt(sx + sy);
         const double S = press ? 40.0 : (shoot ? 120.0 : 100.0);
         const double fdx = S * dx / mag, fdy = S * dy / mag;
         // player velocity: move impulse (f * arrow) / m, or the press impulse
@@ -1811,6 +1876,19 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
     reward[env] = (OT)r;
     done_out[env] = done ? 1 : 0;
     store_env<N>(st, env, B, e);
+    // The clamped-action count (futbol_invalid_actions) is the step's last memory operation, where no
+    // value is live.  It used to follow the action decode, amid ~60 loads in flight and every state
+    // register live: the atomic optimizer turns a divergent atomicAdd into a wave reduction and a
+    // one-lane `if` nested in the `if (bad)`, and at their shared join the register allocator placed
+    // live-range-split copies (v_accvgpr_write aN, vM of per-lane addresses and state) BEFORE the exec
+    // restore, where they run with the inner `if`'s exec mask -- no lane at all when no action was
+    // out of range -- so the AGPRs kept stale values that were read back later: the round-3 wrong
+    // velocities (N = 9), wrong positions and illegal address (N = 7) and the step-19 divergence
+    // (N = 3) of DESIGN.md section 6.  scripts/isa_exec_check.py finds the pattern in the code objects
+    // (tests/test_isa_exec.py).  (Lanes past B returned before the solve: no count.)
+#ifndef FUTBOL_DIAG_EARLY_ATOMIC
+    if (bad) atomicAdd(st.invalid, (unsigned long long)bad);
+#endif
     FUTBOL_CRUMB(L, 99);
     FUTBOL_STAMP(10);
 #ifdef FUTBOL_STAMPS

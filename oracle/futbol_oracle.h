@@ -51,6 +51,7 @@ typedef struct {
     int32_t arb_state[ORC_MAXP];
     int32_t arb_inlist[ORC_MAXP];               /* in last cpSpaceStep's arbiter list */
     double arb_jn[ORC_MAXP];                    /* jnAcc of its (single) contact */
+    uint32_t n_out, n_goal;                     /* diagnostics: out-of-bounds fixes, goals so far */
 } OrcV1;
 
 /* v0 (gym_futbol/envs/futbol_env.py) */
@@ -89,6 +90,9 @@ void orc_v1_vec_step(OrcV1 *envs, int B, const int32_t *actions, double *obs, do
 
 /* C1: one env, nsteps steps in a C loop, synthetic Philox (tag 1) left actions, auto-reset */
 int  orc_v1_run(OrcV1 *e, int nsteps, uint64_t act_seed, double *ret_sum);
+/* cpu_baseline: B envs x nsteps of orc_v1_run's loop, envs split over nthreads OpenMP threads */
+long long orc_v1_vec_run(OrcV1 *envs, int B, int nsteps, uint64_t act_seed, int nthreads, double *ret_sum);
+long long orc_v0_vec_run(OrcV0 *envs, int B, int nsteps, uint64_t act_seed, int nthreads, double *ret_sum);
 
 void orc_v0_init(OrcV0 *e, double length, double width, double goal_size, double game_time,
                  double player_speed, double shoot_speed, int one_goal_end, int only_reward_goal,
@@ -97,6 +101,9 @@ void orc_v0_reset(OrcV0 *e, double *obs);
 int  orc_v0_step(OrcV0 *e, int32_t a0, int32_t a1, double *obs, double *reward);
 void orc_v0_vec_step(OrcV0 *envs, int B, const int32_t *actions, double *obs, double *reward,
                      uint8_t *done, double *terminal_obs, int nthreads);
+
+/* diagnostic: faithful-build squares as x*x at the sites of this mask (futbol_v1_oracle.c) */
+void orc_v1_set_sq_mask(int mask);
 
 /* RNG contract probes (tests) */
 void orc_philox(const uint32_t *ctr, const uint32_t *key, uint32_t *out);

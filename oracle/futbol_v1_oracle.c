@@ -42,16 +42,39 @@
 #define BALL_RADIUS 1.0   /* ball.py:7 */
 #define SEG_RADIUS 1.0    /* futbol_env.py:187.. (last ctor arg) */
 
-/* Python's float `x**2` (libm pow in the faithful build, see oracle_math.h) */
+/* Python's float `x**2`: libm pow in the faithful build (see oracle_math.h) */
+
+/* Diagnostic (tests/sq_divergence.py): the faithful build squares with x*x at the call sites set in
+   this mask instead of pow -- bit 0 get_vec in _process_action (state), bit 1 limit_velocity's
+   Vec2d.length (state), bit 2 the reward's get_vec / _ball_to_team_distance_arr (reward only) --
+   to find which site's difference reaches a discrete outcome.  0 (default): every site faithful. */
+#ifdef ORACLE_PORTABLE
+/* the kernels: glibc's pow(x, 2) restated at the two sites that feed the state (bits 0, 1), x*x at
+   the reward's (bit 2: the reward never feeds back into the state, and its squares' last-bit
+   differences stay below 1e-11) */
+static double SQS(double x, int bit) { return bit == 2 ? x * x : ORC_SQ(x); }
+#else
 static double SQ(double x) { return ORC_SQ_V1(x); }
+static int orc_sq_xx_mask = 0;
+static double SQS(double x, int bit) { return (orc_sq_xx_mask >> bit) & 1 ? x * x : SQ(x); }
+#endif
+void orc_v1_set_sq_mask(int mask)
+{
+#ifndef ORACLE_PORTABLE
+    orc_sq_xx_mask = mask;
+#else
+    (void)mask;
+#endif
+}
 
 /* get_vec, envs_v1/futbol_env.py:56-59: vector from o to t and its magnitude */
-static double get_vec(double tx, double ty, double ox, double oy, double *vx, double *vy)
+static double get_vec_site(double tx, double ty, double ox, double oy, double *vx, double *vy, int bit)
 {
     *vx = tx - ox;
     *vy = ty - oy;
-    return sqrt(SQ(*vx) + SQ(*vy));
+    return sqrt(SQS(*vx, bit) + SQS(*vy, bit));
 }
+#define get_vec(tx, ty, ox, oy, vx, vy) get_vec_site(tx, ty, ox, oy, vx, vy, 0)
 
 static void seg_endpoints(const OrcV1 *e, int s, double *ax, double *ay, double *bx, double *by)
 {
@@ -285,7 +308,7 @@ void orc_v1_space_step(OrcV1 *e, double dt)
     for (int k = 0; k < Nb; ++k) {
         e->vx[k] = e->vx[k] * damping + 0.0 * dt;
         e->vy[k] = e->vy[k] * damping + 0.0 * dt;
-        double l = sqrt(SQ(e->vx[k]) + SQ(e->vy[k])); /* Vec2d.length */
+        double l = sqrt(SQS(e->vx[k], 1) + SQS(e->vy[k], 1)); /* Vec2d.length */
         double vmax = body_vmax(e, k);
         if (l > vmax) {
             double scale = vmax / l;
@@ -501,7 +524,7 @@ static void team_a_dist(const OrcV1 *e, double *d)
 {
     const int ball = 2 * e->N;
     for (int i = 0; i < e->N; ++i)
-        d[i] = sqrt(SQ(e->px[i] - e->px[ball]) + SQ(e->py[i] - e->py[ball]));
+        d[i] = sqrt(SQS(e->px[i] - e->px[ball], 2) + SQS(e->py[i] - e->py[ball], 2));
 }
 
 /* Futbol.step, futbol_env.py:427-483 */
@@ -538,8 +561,8 @@ int orc_v1_step(OrcV1 *e, const int32_t *left, double *obs, double *reward)
         else { mx = diff[0]; for (int i = 1; i < N; ++i) if (diff[i] > mx) mx = diff[i]; }
         r = r + mx * 10;
         double gx = e->width, gy = e->height / 2, t0, t1;
-        double ma = get_vec(e->px[ball], e->py[ball], gx, gy, &t0, &t1);
-        double mi = get_vec(bix, biy, gx, gy, &t0, &t1);
+        double ma = get_vec_site(e->px[ball], e->py[ball], gx, gy, &t0, &t1, 2);
+        double mi = get_vec_site(bix, biy, gx, gy, &t0, &t1, 2);
         r = r + (mi - ma) * 10;
     }
     int goal = 0;
@@ -551,6 +574,8 @@ int orc_v1_step(OrcV1 *e, const int32_t *left, double *obs, double *reward)
         orc_v1_observe(e, o);
         e->owner = oracle_choice(&g, 2);
     }
+    e->n_out += (uint32_t)out;
+    e->n_goal += (uint32_t)goal;
     e->current_time = e->current_time + TIME_STEP;
     int done = e->current_time > e->total_time;
     if (obs) memcpy(obs, o, sizeof(double) * 4 * e->Nb);
@@ -601,6 +626,24 @@ int orc_v1_run(OrcV1 *e, int nsteps, uint64_t act_seed, double *ret_sum)
     }
     *ret_sum = tot;
     return episodes;
+}
+
+/* bench.py cpu_baseline: B envs, each stepped nsteps times by orc_v1_run's loop, envs split over
+   nthreads OpenMP threads (every thread steps its own contiguous block of envs through all nsteps:
+   no per-step fork/join and no Python per step, the fastest schedule of independent envs on a
+   host).  Returns the finished episodes; *ret_sum = the sum of their returns. */
+long long orc_v1_vec_run(OrcV1 *envs, int B, int nsteps, uint64_t act_seed, int nthreads, double *ret_sum)
+{
+    long long eps = 0;
+    double tot = 0.0;
+#pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : 1) reduction(+ : eps, tot)
+    for (int i = 0; i < B; ++i) {
+        double r = 0.0;
+        eps += orc_v1_run(&envs[i], nsteps, act_seed, &r);
+        tot += r;
+    }
+    *ret_sum = tot;
+    return eps;
 }
 
 void orc_philox(const uint32_t *ctr, const uint32_t *key, uint32_t *out) { oracle_philox4x32_10(ctr, key, out); }

@@ -358,10 +358,10 @@ static inline double orc_glibc_pow2(double x)
 
 #ifdef ORACLE_PORTABLE
 /* the kernels' arithmetic: the glibc pow(x, 2.0) and sin / cos restatements above for v0 (the
- * reference-pinned path); envs_v1's Python-level squares (get_vec, _ball_to_team_distance_arr,
- * pymunk's Vec2d.length) are x*x in the envs_v1 kernels -- a deliberate, measured difference from
- * Python's pow: the v1 reference itself is unpinned, and the exact squares
- * would cost the 2v2 step ~50% */
+ * reference-pinned path) and for envs_v1's squares that feed the state (_process_action's get_vec,
+ * pymunk's Vec2d.length in limit_velocity: futbol_v1_oracle.c SQS); the envs_v1 reward's squares
+ * (get_vec, _ball_to_team_distance_arr) stay x*x in the kernels -- a deliberate, measured
+ * difference from Python's pow in the reward's last bits only */
 #define ORC_SQ(x) orc_glibc_pow2(x)
 #define ORC_SQ_V1(x) ((x) * (x))
 #define ORC_SIN(x) orc_glibc_sin(x)

@@ -1,0 +1,110 @@
+"""Static check of the built gfx950 code objects for one miscompilation pattern (DESIGN.md section 6,
+"compiler"): register copies placed at the start of a join block BEFORE its exec-mask restore.
+
+A divergent `if` is lowered to `s_and_saveexec_b64 sX, ...` / `s_cbranch_execz JOIN` / body / `JOIN:
+s_or_b64 exec, exec, sX`.  Any vector instruction between the JOIN label and the restore executes with
+the body's lanes only -- with NO lane when the execz branch was taken.  A register-allocator copy of
+a value that is live in every lane (a live-range split: `v_accvgpr_write aN, vM`, `v_mov`, a scratch
+spill) placed there leaves the destination stale in the other lanes, and whatever later reads it back
+gets garbage.  Found in round 4 in the N = 9 step instances built with max-memory-clause scheduling
+and 8 preloaded cache entries: the per-lane address of an arbiter-cache array copied into a144:a145
+at the join of the invalid-action atomic's `if`, and read back 1 600 instructions later.
+
+usage: python scripts/isa_exec_check.py <object.o | code-object.elf> ...   (exit 1 on findings)
+       check_object(path) -> [(kernel, join_address, [instructions])]
+"""
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+COPY = re.compile(r"(v_accvgpr_write|v_accvgpr_read|v_accvgpr_mov|v_mov_b32|v_mov_b64|scratch_store|scratch_load|"
+                  r"buffer_store|buffer_load)")
+RESTORE = re.compile(r"s_or_b64 exec, exec, s\[\d+:\d+\]")
+LINE = re.compile(r"^\s+(\S.*?)\s*//\s*([0-9A-F]+):")
+FUNC = re.compile(r"^([0-9a-f]+) <(\S+)>:")
+
+
+def code_objects(path):
+    """gfx950 code object(s) of a HIP object file (its .hip_fatbin bundle), or the path itself if it is
+    already an AMDGPU ELF."""
+    out = subprocess.run([LLVM + "/llvm-readelf", "-h", path], capture_output=True, text=True).stdout
+    if "AMDGPU" in out:
+        return [path]
+    secs = subprocess.run([LLVM + "/llvm-readelf", "-S", path], capture_output=True, text=True).stdout
+    if ".hip_fatbin" not in secs:
+        return []  # host code only
+    tmp = tempfile.mkdtemp(prefix="isa_")
+    fb = os.path.join(tmp, "fatbin")
+    subprocess.run([LLVM + "/llvm-objcopy", "--dump-section=.hip_fatbin=" + fb, path, os.path.join(tmp, "x.o")],
+                   check=True, capture_output=True)
+    co = os.path.join(tmp, "gfx950.elf")
+    subprocess.run([LLVM + "/clang-offload-bundler", "--type=o", "--input=" + fb,
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", "--output=" + co, "--unbundle"],
+                   check=True, capture_output=True)
+    return [co]
+
+
+def scan(disasm):
+    """findings of one llvm-objdump -d listing"""
+    cur = None
+    ins = []  # (addr, kernel, text)
+    for ln in disasm.splitlines():
+        m = FUNC.match(ln)
+        if m:
+            cur = m.group(2)
+            continue
+        m = LINE.match(ln)
+        if m and cur:
+            ins.append((int(m.group(2), 16), cur, m.group(1)))
+    index = {a: i for i, (a, _, _) in enumerate(ins)}
+    starts, execz = set(), set()
+    for a, k, t in ins:
+        if t.startswith(("s_cbranch", "s_branch")):
+            # SOPP branch: target = address + 4 + 4 * simm16
+            off = int(t.split()[1])
+            tgt = a + 4 + 4 * (off - 65536 if off >= 32768 else off)
+            starts.add(tgt)
+            if t.startswith("s_cbranch_execz"):
+                execz.add(tgt)
+    found = []
+    for tgt in sorted(execz):
+        i = index.get(tgt)
+        if i is None:
+            continue
+        pre = []
+        for a, k, t in ins[i:i + 64]:
+            if a != tgt and a in starts:
+                break
+            if RESTORE.match(t):
+                c = [p for p in pre if COPY.match(p)]
+                if c:
+                    found.append((k, hex(tgt), c))
+                break
+            dst = t.split(",")[0]
+            if "exec" in dst or "saveexec" in t or t.startswith(("s_cbranch", "s_branch", "s_endpgm")):
+                break
+            pre.append(re.sub(r"\s+", " ", t))
+    return found
+
+
+def check_object(path):
+    found = []
+    for co in code_objects(path):
+        dis = subprocess.run([LLVM + "/llvm-objdump", "-d", "--no-show-raw-insn", co], capture_output=True,
+                             text=True, check=True).stdout
+        found += scan(dis)
+    return found
+
+
+if __name__ == "__main__":
+    bad = 0
+    for p in sys.argv[1:]:
+        f = check_object(p)
+        print("%-40s %d finding(s)" % (os.path.basename(p), len(f)))
+        for k, a, c in f:
+            print("   %s @ %s: %s" % (k[:70], a, "; ".join(c[:4])))
+        bad += len(f)
+    sys.exit(1 if bad else 0)

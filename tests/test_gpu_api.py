@@ -296,3 +296,25 @@ def test_rollout_equals_steps(env_id, B, K):
     assert int(done.sum()) >= B  # an episode end inside the rollout
     a.close()
     b.close()
+
+
+def test_rollout_rejects_bad_out_buffers():
+    """rollout(out=...) hands raw pointers to the kernel: a buffer of the wrong dtype, a shorter K,
+    a non-contiguous view or a CPU tensor is refused before the launch."""
+    env = gf.make("Futbol2v2-v1", num_envs=128, seed=4)
+    env.reset()
+    acts = env.random_actions_steps(6, 0, seed=5)
+    good = env.rollout(acts)
+    bad = [
+        (good[0].to(torch.float64 if good[0].dtype == torch.float32 else torch.float32),) + good[1:],
+        (good[0][:5],) + good[1:],
+        (good[0], good[1], good[2][:, ::2].contiguous(), good[3]),
+        (good[0], good[1].t().contiguous().t(), good[2], good[3]),
+        (good[0].cpu(),) + good[1:],
+        good[:3],
+    ]
+    for out in bad:
+        with pytest.raises(ValueError):
+            env.rollout(acts, out=out)
+    env.rollout(acts, out=good)  # the right buffers are accepted
+    env.close()
