@@ -114,6 +114,29 @@ def cpu_threads():
     return max(1, os.cpu_count() or 1)
 
 
+def cpu_quota():
+    """The CPU time this process's cgroup may use, in CPUs (cgroup v2 cpu.max or v1 cfs quota), or None
+    when unlimited / unknown.  (The GPU box's affinity mask lists all 256 host CPUs, but its share is a
+    quota: 256 threads there ran at 11.6 M env-steps/s against 26.5 M on 16.)"""
+    import math
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                return max(1, math.ceil(int(q) / int(per)))
+            return None
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return max(1, math.ceil(q / per)) if q > 0 else None
+    except (OSError, ValueError):
+        return None
+
+
 def omp_share():
     """OMP_NUM_THREADS when set (16 on the GPU box: its CPU share per GPU), else None."""
     try:
@@ -155,14 +178,20 @@ def cpu_baseline(kind, n, budget_s=8.0, B=65536):
     T = cpu_threads()
     allc = timed(T)
     share = omp_share()
+    quota = cpu_quota()
     sh = timed(share) if share and share != T else None
+    qt = timed(quota) if quota and quota not in (T, share) else None
     one = timed(1) if T > 1 else allc
-    out = {"value": allc["value"], "unit": "env-steps/s", "cores": T, "kind": "port",
+    # the baseline is the host's best: every core of the affinity mask, or the cgroup's CPU quota / the
+    # OMP_NUM_THREADS share when the mask lists more CPUs than the process may use (all reported)
+    best = max([r for r in (allc, sh, qt) if r], key=lambda r: r["value"])
+    out = {"value": best["value"], "unit": "env-steps/s", "cores": best["threads"], "kind": "port",
            "sample": "oracle/liboracle.so (C restatement of the %s step), %d envs x %d steps (%.1f s) on %d OpenMP "
-                     "threads = every core of the affinity mask; each thread steps its own envs in a C loop "
-                     "(synthetic Philox actions, auto-reset)" % (what, B, allc["steps"], allc["seconds"], T),
-           "all_cores": allc, "omp_share": sh, "single_thread": one, "single_thread_value": one["value"],
-           "host": host_cpu(), "reference_v0_python": REF_V0_PYTHON}
+                     "threads (the fastest of: all %d CPUs of the affinity mask, the OMP_NUM_THREADS share %s, the "
+                     "cgroup quota %s); each thread steps its own envs in a C loop (synthetic Philox actions, "
+                     "auto-reset)" % (what, B, best["steps"], best["seconds"], best["threads"], T, share, quota),
+           "all_cores": allc, "omp_share": sh, "cgroup_quota_cpus": quota, "quota_run": qt, "single_thread": one,
+           "single_thread_value": one["value"], "host": host_cpu(), "reference_v0_python": REF_V0_PYTHON}
     if kind == "v1" and n == 2:
         out["c1"] = c1_baseline(n)
     return out

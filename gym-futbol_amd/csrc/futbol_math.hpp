@@ -423,22 +423,29 @@ __host__ __device__ __forceinline__ void glibc_pow2_batch(const double (&x)[M], 
     }
 }
 
-// Copy the pow tables (kPowLog, then kPowExp: 5 KB) into `lds` with every lane of a one-wave block,
-// 16 bytes per lane and access (lanes 0..63: 5 loads, no dependence between them); returns the LDS
-// copies' addresses.  The caller has the wave converged, and `lds` 16-byte aligned and not in use.
+// Copy the pow tables (kPowLog, then kPowExp: 5 KB) into `lds` with the wave's active lanes (16 bytes
+// per lane and access: the active lanes stride over the 320 chunks, so a partial wave -- the lanes past
+// B of the last block have returned, a restart phase runs on some lanes only -- copies all of them);
+// returns the LDS copies' addresses.  `lds` is 16-byte aligned and not in use; one-wave blocks.
 __device__ __forceinline__ void stage_pow_tables(void* lds, const double*& logt, const uint64_t*& expt)
 {
     const uint4* sl = reinterpret_cast<const uint4*>(kPowLog);
     const uint4* se = reinterpret_cast<const uint4*>(kPowExp);
     uint4* d = reinterpret_cast<uint4*>(lds);
     constexpr int NL = (int)sizeof(kPowLog) / 16, NE = (int)sizeof(kPowExp) / 16;  // 192, 128
-    const int l = (int)(threadIdx.x & 63u);
-    const uint4 a0 = sl[l], a1 = sl[l + 64], a2 = sl[l + 128], b0 = se[l], b1 = se[l + 64];
-    d[l] = a0;
-    d[l + 64] = a1;
-    d[l + 128] = a2;
-    d[NL + l] = b0;
-    d[NL + l + 64] = b1;
+    const uint64_t live = __ballot(1);
+    const int A = __popcll(live);
+    const int w = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
+    if (A == 64) {  // the common case: five independent loads per lane
+        const uint4 a0 = sl[w], a1 = sl[w + 64], a2 = sl[w + 128], b0 = se[w], b1 = se[w + 64];
+        d[w] = a0;
+        d[w + 64] = a1;
+        d[w + 128] = a2;
+        d[NL + w] = b0;
+        d[NL + w + 64] = b1;
+    } else {
+        for (int i = w; i < NL + NE; i += A) d[i] = i < NL ? sl[i] : se[i - NL];
+    }
     static_assert(NL == 192 && NE == 128, "5 uint4 per lane");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -500,7 +507,13 @@ __device__ __forceinline__ void glibc_pow2_need_lds(const double (&x)[M], double
     if (__builtin_expect(__ballot(pend != 0u) != 0ull, 0)) {  // wave-uniform
         const double* logt;
         const uint64_t* expt;
+#ifdef FUTBOL_DIAG_POW_GLOBAL  // diagnostic builds only: the tables read from global memory
+        (void)lds;
+        logt = kPowLog;
+        expt = kPowExp;
+#else
         stage_pow_tables(lds, logt, expt);
+#endif
         while (pend != 0u) {
             const uint64_t bit = pend & (0ull - pend);
             double v = 0.0;
@@ -511,6 +524,13 @@ __device__ __forceinline__ void glibc_pow2_need_lds(const double (&x)[M], double
             for (int i = 0; i < M; ++i) h[i] = bit == (1ull << i) ? f : h[i];
             pend &= pend - 1u;
         }
+        // The caller reuses this LDS with other types next (the solver rows are double2): without a
+        // barrier here, type-based alias analysis may move those stores above the last u64 / double
+        // table reads (it did: the N = 6 f64 runtime-geometry rollout instance read positions as
+        // exp-table entries from step 18 on, with LLVM's default scheduler)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
 }
 

@@ -151,11 +151,22 @@ constexpr bool kSolveComponents = 2 * N + 1 <= 8;
 #ifndef FUTBOL_K5
 #define FUTBOL_K5 4
 #endif
+// One set of solver rows (N >= FUTBOL_ONE_ROWS_MIN, round 4): the LDS holds Nb + 1 rows per lane
+// instead of 2 Nb + 1 -- the narrowphase stages positions, then velocities, in the same rows (each
+// record's bounce is a second pass over the contact work list), and the split solve runs the v half
+// and then the v_bias half on them.  It brings N = 8..10 from 3 one-wave blocks per CU (53 KB of LDS
+// each: 65 536 envs in two rounds of waves) to 4 (one round); the halves cost nothing extra there, since
+// 2 x (envs with contacts) items took two rounds of the wave's lanes anyway.
+#ifndef FUTBOL_ONE_ROWS_MIN
+#define FUTBOL_ONE_ROWS_MIN 8
+#endif
 template <int N>
 struct V1Shape {
     static constexpr int Nb = 2 * N + 1;
     static constexpr int BALL = 2 * N;
     static constexpr int P = v1_npairs(N);
+    static constexpr bool ONE_ROWS = N >= FUTBOL_ONE_ROWS_MIN;
+    static constexpr int NROWS = ONE_ROWS ? Nb + 1 : 2 * Nb + 1;
     // LDS contact-record slots per lane: 4 one-wave blocks per CU must fit in 160 KB
     // (40 KB per block: K * 4 KB of records + (2 Nb + 1) KB of solver velocity rows + the segment table)
     // for N <= 7; N = 8, 9, 10 (the rows alone take 35-43 KB) fit 3 blocks per CU (53 KB each)
@@ -197,7 +208,8 @@ struct Scratch {
     // as rows[0] + off (h = 0) or rows[2 Nb] - off (h = 1): both halves reach Z with no select.
     // During the narrowphase the same rows stage the bodies' positions (v_bias rows) and
     // velocities (v rows) for the per-lane dynamic body index.
-    double2 rows[2 * S::Nb + 1][EPW];
+    // (S::ONE_ROWS: rows[k] is body k's v, then v_bias, in turn; Z = rows[Nb])
+    double2 rows[S::NROWS][EPW];
     double minv[S::Nb + 1];  // inverse mass by row: players, ball, Z = 0
     // split solve work list (+ a spare entry): env column (6 bits) | LDS record slots (8) << 6 | dt code of
     // the env's previous cpSpaceStep (warm-start dt ratio, 2) << 14 | the env's record count << 16
@@ -205,7 +217,7 @@ struct Scratch {
     SegLds seg[kNSeg];
 
     __device__ __forceinline__ double2& vb(int k, int l) { return rows[k][l]; }
-    __device__ __forceinline__ double2& v(int k, int l) { return rows[2 * S::Nb - k][l]; }
+    __device__ __forceinline__ double2& v(int k, int l) { return rows[S::ONE_ROWS ? k : 2 * S::Nb - k][l]; }
 };
 
 // info word (64 bits, stored as the bits of a double; only the low 32 are used):
@@ -510,7 +522,7 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
     sfor<S::Nb>([&](auto K) {
         constexpr int k = K;
         sh_->vb(k, ln_) = make_double2(e.px[k], e.py[k]);
-        sh_->v(k, ln_) = make_double2(e.vx[k], e.vy[k]);
+        if constexpr (!S::ONE_ROWS) sh_->v(k, ln_) = make_double2(e.vx[k], e.vy[k]);
     });
     // collide in canonical order; cpArbiterUpdate + preStep folded in (needs pre-damping v)
     int n = 0;
@@ -689,7 +701,10 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
         const int a = segc ? as : i;
         const int sg = segc ? pid - as * kNSeg : 0;
         const int j = segc ? a : q - (i * S::Nb - i * (i + 1) / 2) + i + 1;  // (segment: any valid row)
-        const double2 pa = sh_->vb(a, o), va = sh_->v(a, o), pb = sh_->vb(j, o), vbj = sh_->v(j, o);
+        // (S::ONE_ROWS: the rows hold positions only now; the bounce is the second pass below)
+        const double2 pa = sh_->vb(a, o), pb = sh_->vb(j, o);
+        const double2 va = S::ONE_ROWS ? make_double2(0.0, 0.0) : sh_->v(a, o);
+        const double2 vbj = S::ONE_ROWS ? make_double2(0.0, 0.0) : sh_->v(j, o);
         const SegLds g = sh_->seg[sg];
         double qx, qy;
         seg_closest(pa.x, pa.y, g.ax, g.ay, g.sdx, g.sdy, g.L2, g.rL2, qx, qy);
@@ -758,6 +773,39 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
             sp0[3] = q3;
         }
     };
+    // S::ONE_ROWS: the bounce of record r of env column o (hit pid), from the velocities staged over
+    // the positions -- CircleToSegment / CircleToCircle's bounce expression of `contact`, unchanged
+    auto bounce_rec = [&](int o, int oenv, int pid, int r) {
+        const bool segc = pid < S::Nb * kNSeg;
+        const int q = pid - S::Nb * kNSeg;
+        int i = 0;
+        sfor<1, S::Nb - 1>([&](auto K) {
+            constexpr int k = K;
+            i += q >= k * S::Nb - k * (k + 1) / 2 ? 1 : 0;
+        });
+        const int a = segc ? pid / kNSeg : i;
+        const int j = segc ? a : q - (i * S::Nb - i * (i + 1) / 2) + i + 1;
+        const double2 va = sh_->v(a, o), vbj = sh_->v(j, o);
+        const double bvx_ = segc ? 0.0 : vbj.x, bvy_ = segc ? 0.0 : vbj.y;
+        const double ee = segc ? kE * 0.0 : kE * kE;
+        double* sp_ = r < KLs ? nullptr : L.spill + ((size_t)oenv * (S::P - KLs) + (r - KLs)) * 8;
+        const double2 nn = r < KLs ? sh_->rec[r][0][o] : *(const double2*)sp_;
+        const double bounce = ((bvx_ - va.x) * nn.x + (bvy_ - va.y) * nn.y) * ee;
+        if (r < KLs) sh_->rec[r][2][o].y = -bounce;
+        else sp_[5] = -bounce;
+    };
+    auto stage_velocities = [&]() {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        sfor<S::Nb>([&](auto K) {
+            constexpr int k = K;
+            sh_->v(k, ln_) = make_double2(e.vx[k], e.vy[k]);
+        });
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
     n = nh;
     if (dtc == 2) {
         FUTBOL_STAT(26, total);
@@ -798,6 +846,14 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
             const uint32_t en = table[it];
             const int o = (int)(en & 63u);
             contact(o, env - ln_ + o, (int)((en >> 6) & 1023u), (int)(en >> 16), false);
+        }
+        if constexpr (S::ONE_ROWS) {  // velocities over the positions (row Z keeps the table), bounces
+            stage_velocities();
+            for (uint32_t it = w0; it < total; it += A) {
+                const uint32_t en = table[it];
+                const int o = (int)(en & 63u);
+                bounce_rec(o, env - ln_ + o, (int)((en >> 6) & 1023u), (int)(en >> 16));
+            }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -842,6 +898,28 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
                 ++r;
             }
         });
+        if constexpr (S::ONE_ROWS) {  // velocities over the positions, then this lane's bounces
+            stage_velocities();
+            int r2 = 0;
+            sfor<NWS>([&](auto WD) {
+                uint64_t h = hsw[WD];
+                while (h) {
+                    const int bit = __builtin_ctzll(h);
+                    h &= h - 1;
+                    bounce_rec(ln_, env, pid_of(WD, bit, true), r2);
+                    ++r2;
+                }
+            });
+            sfor<NPW>([&](auto Q) {
+                uint64_t h = hpw[Q];
+                while (h) {
+                    const int bit = __builtin_ctzll(h);
+                    h &= h - 1;
+                    bounce_rec(ln_, env, pid_of(Q, bit, false), r2);
+                    ++r2;
+                }
+            });
+        }
     }
 
     FUTBOL_CRUMB(L, 40 + dtc);
@@ -986,7 +1064,7 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
             sfor<S::Nb>([&](auto K) {
                 constexpr int k = K;
                 sh->v(k, ln) = make_double2(e.vx[k], e.vy[k]);
-                sh->vb(k, ln) = make_double2(0.0, 0.0);
+                if constexpr (!S::ONE_ROWS) sh->vb(k, ln) = make_double2(0.0, 0.0);
             });
             sh->rows[S::Nb][ln] = make_double2(0.0, 0.0);
             {
@@ -1004,21 +1082,42 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             FUTBOL_STAMP(dtc == 2 ? 19 : 9);
-            const int items = 2 * total;
+            // two row sets: one pass, items (env / component, half) with the halves on different lanes;
+            // S::ONE_ROWS: pass 0 runs the v halves on the v rows, pass 1 the v_bias halves on the same
+            // rows (re-staged as v_bias = +0), one item per env / component per pass
+            constexpr int NPASS = S::ONE_ROWS ? 2 : 1;
+            const int items = S::ONE_ROWS ? total : 2 * total;
             constexpr uint32_t ROW = EPW * (uint32_t)sizeof(double2);
             const double coef2 = dt / P.dtv[2], coef1 = dt / P.dtv[1];  // dt / prev_dt, prev_dt != 0
+#pragma unroll 1
+            for (int pass = 0; pass < NPASS; ++pass) {
+            if (S::ONE_ROWS && pass == 1) {  // the v results out, v_bias = +0 in
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                sfor<S::Nb>([&](auto K) {
+                    constexpr int k = K;
+                    const double2 v = sh->v(k, ln);
+                    e.vx[k] = v.x;
+                    e.vy[k] = v.y;
+                    sh->vb(k, ln) = make_double2(0.0, 0.0);
+                });
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
             for (int i0 = 0; i0 < items; i0 += A) {
                 const int it_ = i0 + w;
                 if (it_ < items) {
-                    const uint32_t ent = sh->item[it_ >> 1];
+                    const uint32_t ent = sh->item[S::ONE_ROWS ? it_ : it_ >> 1];
                     const int ie = (int)(ent & 63u);
-                    const int h = it_ & 1;
+                    const int h = S::ONE_ROWS ? 1 - pass : it_ & 1;
                     // cpArbiterApplyCachedImpulse's dt ratio of THIS env (its previous step may have
                     // been a 1e-4 reset micro-step)
                     const uint32_t ipc = (ent >> 14) & 3u;
                     const double dt_coef = ipc == 2 ? coef2 : (ipc == 1 ? coef1 : 0.0);
-                    char* const base = (char*)&sh->rows[h ? 2 * S::Nb : 0][ie];
-                    const int sgn = h ? -1 : 1;
+                    char* const base = (char*)&sh->rows[S::ONE_ROWS ? 0 : (h ? 2 * S::Nb : 0)][ie];
+                    const int sgn = S::ONE_ROWS ? 1 : (h ? -1 : 1);
                     const double* const mtab = sh->minv;
                     auto row = [&](uint32_t off) { return (double2*)(base + sgn * (int)off); };
                     auto mass = [&](uint32_t off) { return mtab[off / ROW]; };
@@ -1169,15 +1268,19 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
                     }
                 }
             }
+            }  // passes
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             // (a lane without contacts reads back the v it published and v_bias = +0)
             sfor<S::Nb>([&](auto K) {
                 constexpr int k = K;
-                const double2 v = sh->v(k, ln), vb = sh->vb(k, ln);
-                e.vx[k] = v.x;
-                e.vy[k] = v.y;
+                const double2 vb = sh->vb(k, ln);
+                if constexpr (!S::ONE_ROWS) {
+                    const double2 v = sh->v(k, ln);
+                    e.vx[k] = v.x;
+                    e.vy[k] = v.y;
+                }
                 e.bx[k] = vb.x;
                 e.by[k] = vb.y;
             });
@@ -1450,6 +1553,9 @@ __device__ __forceinline__ void do_reset(const V1Params& P, const V1Params* __re
 // players: more lanes with a second passer, more registers), N >= 6 keeps the blocks in the branch
 template <int N>
 constexpr bool kPassDraws = N >= 3 && N <= 5;
+#ifndef FUTBOL_PA_SPLIT  // _process_action's player loop in three passes (v1_step_body)
+#define FUTBOL_PA_SPLIT 0
+#endif
 struct PassDraws {
     uint32_t j0;
     uint32_t a0, b0, a1, b1;  // words 0 and 1 of the blocks at j0 and j0 + 1 (all choice_of reads)
@@ -1466,6 +1572,53 @@ struct PassDraws {
         return k > n - 1 ? n - 1 : k;
     }
 };
+
+// the teammate index (0..N-1 within the side) chosen by get_pass_target_teammate: the draws only
+template <int N, int side, int me>
+__device__ __forceinline__ int pass_choice(const Env<N>& e, Stream& rs, PassDraws& pd, int ar)
+{
+    constexpr int base = side * N;
+    if constexpr (N == 1) {
+        return 0;
+    } else {
+        int t;
+        if constexpr (N - 1 == 1) {
+            rs.skip(1);
+            t = 0;
+        } else {
+            t = kPassDraws<N> ? pd.choice(rs, N - 1) : rs.choice(N - 1);
+        }
+        t = t >= me ? t + 1 : t;
+        if (ar != 0) {
+            const double x0 = e.px[base + me], y0 = e.py[base + me];
+            auto dir_ok = [&](double mx, double my) {
+                return ((ar == 1) & (my > 0)) | ((ar == 2) & (mx > 0)) | ((ar == 3) & (my < 0)) | ((ar == 4) & (mx < 0));
+            };
+            int cnt = 0;
+            sfor<N>([&](auto Q) {
+                constexpr int q = Q;
+                cnt += dir_ok(e.px[base + q] - x0, e.py[base + q] - y0) ? 1 : 0;
+            });
+            if (cnt > 0) {
+                int pick;
+                if constexpr (N - 1 == 1) {
+                    rs.skip(1);
+                    pick = 0;
+                } else {
+                    pick = kPassDraws<N> ? pd.choice(rs, cnt) : rs.choice(cnt);
+                }
+                sfor<N>([&](auto Q) {
+                    constexpr int q = Q;
+                    if (dir_ok(e.px[base + q] - x0, e.py[base + q] - y0)) {
+                        if (pick == 0) t = q;
+                        --pick;
+                    }
+                });
+            }
+        }
+        return t;
+    }
+}
 
 template <int N, int side, int me>
 __device__ __forceinline__ void pass_target(const Env<N>& e, Stream& rs, PassDraws& pd, int ar, double& tx, double& ty,
@@ -1696,6 +1849,93 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
                   ((uint64_t)(shoot_side != 0) << (4 * N + 2));
     }
     glibc_pow2_need_lds<NSQ>(sqin, sq, sqneed, &sh.rows[0][0]);  // (rows: unused until space_step)
+#if FUTBOL_PA_SPLIT
+    // The loop in three passes, same arithmetic and draw order: only the ball's velocity (dribble,
+    // kick) and the owner carry from one player to the next -- a player's own velocity, its direction
+    // d and the quotients S * d / |d| depend on the positions alone.  (A) the pass targets, in player
+    // order (their draws, with the divergent branches of the N >= 3 choice); (B) every player's sqrt and
+    // two divisions and its own velocity, in one basic block, so that the scheduler overlaps the 2N
+    // independent quotient chains; (C) the ball's velocity chain and the owner, in player order.
+    int tgt[2 * N];
+    sfor<2 * N>([&](auto K) {
+        constexpr int k = K;
+        constexpr int side = k < N ? 0 : 1;
+        const int ar = arrow[k];
+        const bool pass = (key[k] == 4) & touch[k];
+        if constexpr (N == 2) {
+            constexpr int mate = side * N + (1 - (k - side * N));
+            const double mx = e.px[mate] - e.px[k], my = e.py[mate] - e.py[k];
+            const bool way = ((ar == 1) & (my > 0)) | ((ar == 2) & (mx > 0)) | ((ar == 3) & (my < 0)) | ((ar == 4) & (mx < 0));
+            rs.skip(pass ? (way ? 2u : 1u) : 0u);
+            tgt[k] = mate - side * N;
+        } else {
+            tgt[k] = 0;
+            if (pass) tgt[k] = pass_choice<N, side, k - side * N>(e, rs, pd, ar);
+        }
+    });
+    double fdxa[2 * N], fdya[2 * N];
+    sfor<2 * N>([&](auto K) {
+        constexpr int k = K;
+        constexpr int side = k < N ? 0 : 1;
+        constexpr int base = side * N;
+        const int ar = arrow[k], ky = key[k];
+        const bool tk = touch[k];
+        const int fx = ar == 2 ? 1 : (ar == 4 ? -1 : 0);
+        const int fy = ar == 1 ? 1 : (ar == 3 ? -1 : 0);
+        const bool move = ky <= 1;
+        const bool shoot = (ky == 2) & tk;
+        const bool press = (ky == 3) & !tk & (ar == 0);
+        double tx, ty, tsx, tsy;  // the pass target's position and squares (exact selects, see pass_target)
+        if constexpr (N == 2) {
+            constexpr int mate = side * N + (1 - (k - side * N));
+            tx = e.px[mate];
+            ty = e.py[mate];
+            tsx = sq[2 * mate];
+            tsy = sq[2 * mate + 1];
+        } else {
+            tx = 0.0;
+            ty = 0.0;
+            tsx = 0.0;
+            tsy = 0.0;
+            sfor<N>([&](auto Q) {
+                constexpr int q = Q;
+                const double sel = q == tgt[k] ? 1.0 : 0.0;
+                tx = __builtin_fma(sel, e.px[base + q], tx);
+                ty = __builtin_fma(sel, e.py[base + q], ty);
+                tsx = __builtin_fma(sel, sq[2 * (base + q)], tsx);
+                tsy = __builtin_fma(sel, sq[2 * (base + q) + 1], tsy);
+            });
+        }
+        const double gx = side == 0 ? W : 0.0, gy = H / 2;
+        const double ox = press ? e.px[k] : e.px[BL], oy = press ? e.py[k] : e.py[BL];
+        const double qx = press ? e.px[BL] : (shoot ? gx : tx), qy = press ? e.py[BL] : (shoot ? gy : ty);
+        const double dx = qx - ox, dy = qy - oy;
+        const double sx = press ? sq[2 * k] : (shoot ? sq[4 * N + side] : tsx);
+        const double sy = press ? sq[2 * k + 1] : (shoot ? sq[4 * N + 2] : tsy);
+        const double mag = sqrt(sx + sy);
+        const double S = press ? 40.0 : (shoot ? 120.0 : 100.0);
+        fdxa[k] = S * dx / mag;
+        fdya[k] = S * dy / mag;
+        const int f = ky == 0 ? 20 : 40;
+        const double mvx = e.vx[k] + (double)(f * fx) * kPlayerMinv, mvy = e.vy[k] + (double)(f * fy) * kPlayerMinv;
+        const double pvx = e.vx[k] + fdxa[k] * kPlayerMinv, pvy = e.vy[k] + fdya[k] * kPlayerMinv;
+        e.vx[k] = move ? mvx : (press ? pvx : e.vx[k]);
+        e.vy[k] = move ? mvy : (press ? pvy : e.vy[k]);
+    });
+    sfor<2 * N>([&](auto K) {
+        constexpr int k = K;
+        constexpr int side = k < N ? 0 : 1;
+        const int ky = key[k];
+        const bool tk = touch[k];
+        const bool move = ky <= 1, shoot = (ky == 2) & tk, pass = (ky == 4) & tk;
+        const double D = shoot ? 2.0 : 10.0, rD = shoot ? 0.5 : 0.1;
+        const double kvx = cdiv(e.vx[BL], D, rD) + fdxa[k] * kBallMinv, kvy = cdiv(e.vy[BL], D, rD) + fdya[k] * kBallMinv;
+        const bool dribble = move & tk, kick = shoot | pass;
+        e.vx[BL] = dribble ? e.vx[k] : (kick ? kvx : e.vx[BL]);
+        e.vy[BL] = dribble ? e.vy[k] : (kick ? kvy : e.vy[BL]);
+        owner = tk ? (uint32_t)side : owner;
+    });
+#else
     sfor<2 * N>([&](auto K) {
         constexpr int k = K;
         constexpr int side = k < N ? 0 : 1;
@@ -1751,6 +1991,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
         e.vy[BL] = dribble ? e.vy[k] : (kick ? kvy : e.vy[BL]);
         owner = tk ? (uint32_t)side : owner;
     });
+#endif
 
     // check_and_fix_out_bounds (:247-287), before physics
     bool out = false;
@@ -1925,8 +2166,9 @@ __global__ void __launch_bounds__(EPW) FUTBOL_V1_STEP_ATTR v1_step_kernel(const 
                                                       OT* __restrict__ reward, uint8_t* __restrict__ done_out,
                                                       OT* __restrict__ term_obs, int nsteps)
 {
-    // 4 blocks per CU (160 KB of LDS) up to N = 7, 3 blocks beyond
-    static_assert(sizeof(Scratch<N, EPW>) <= (N <= 7 ? 160 * 1024 / 4 : 160 * 1024 / 3), "LDS per block");
+    // 4 blocks per CU (160 KB of LDS) up to N = 7 and with one row set, 3 blocks otherwise
+    static_assert(sizeof(Scratch<N, EPW>) <= (N <= 7 || V1Shape<N>::ONE_ROWS ? 160 * 1024 / 4 : 160 * 1024 / 3),
+                  "LDS per block");
     __shared__ Scratch<N, EPW> sh;
     using S = V1Shape<N>;
     if constexpr (!ROLL) {

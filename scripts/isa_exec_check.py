@@ -70,6 +70,15 @@ def scan(disasm):
             if t.startswith("s_cbranch_execz"):
                 execz.add(tgt)
     found = []
+    # blocks entered with a possibly partial / empty exec mask: execz-branch targets (the join of a
+    # skipped branch) and the fallthrough of a loop's backward s_cbranch_execnz (the loop exit: every
+    # lane has left the loop, exec = 0 until the exit's restore)
+    for a, k, t in ins:
+        if t.startswith("s_cbranch_execnz"):
+            off = int(t.split()[1])
+            if off >= 32768:  # backward branch: a loop
+                execz.add(a + 4)
+                starts.add(a + 4)
     for tgt in sorted(execz):
         i = index.get(tgt)
         if i is None:

@@ -43,12 +43,15 @@ def test_cpu_baseline_record(kind, monkeypatch):
     monkeypatch.setenv("OMP_NUM_THREADS", "2")
     r = bench.cpu_baseline(kind, 2, budget_s=0.2, B=256)
     T = len(os.sched_getaffinity(0))
-    assert r["unit"] == "env-steps/s" and r["kind"] == "port" and r["cores"] == T
-    assert r["all_cores"]["threads"] == T and r["value"] == r["all_cores"]["value"] > 0
+    assert r["unit"] == "env-steps/s" and r["kind"] == "port"
+    assert r["all_cores"]["threads"] == T and r["all_cores"]["value"] > 0
     assert r["single_thread"]["threads"] == 1 and r["single_thread_value"] > 0
     if T != 2:
         assert r["omp_share"]["threads"] == 2 and r["omp_share"]["value"] > 0
-    assert "%d OpenMP threads" % T in r["sample"]
+    runs = [x for x in (r["all_cores"], r["omp_share"], r["quota_run"]) if x]
+    best = max(runs, key=lambda x: x["value"])  # the reported baseline is the host's best configuration
+    assert r["value"] == best["value"] and r["cores"] == best["threads"]
+    assert "%d OpenMP threads" % r["cores"] in r["sample"]
     assert r["host"]["nproc"] >= 1 and "reference_v0_python" in r
     if kind == "v1":
         c1 = r["c1"]  # 1 env, 1 thread, 100 000 steps
