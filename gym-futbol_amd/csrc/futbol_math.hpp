@@ -436,6 +436,11 @@ __device__ __forceinline__ void stage_pow_tables(void* lds, const double*& logt,
     const uint64_t live = __ballot(1);
     const int A = __popcll(live);
     const int w = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
+    // the LDS held double2 rows until now: keep these stores after every earlier access to it (type-based
+    // alias analysis would otherwise be free to move them up, see glibc_pow2_need_lds)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (A == 64) {  // the common case: five independent loads per lane
         const uint4 a0 = sl[w], a1 = sl[w + 64], a2 = sl[w + 128], b0 = se[w], b1 = se[w + 64];
         d[w] = a0;

@@ -80,6 +80,11 @@ constexpr int CBN = N >= 5 ? 1 : 4;
 // (N = 6..10 share one count; N = 1, 3, 4 rarely spill: none)
 template <int N>
 constexpr int KXN = N == 5 ? FUTBOL_SPILL_REGS : (N >= 6 ? FUTBOL_SPILL_REGS_BIG : (N == 2 ? FUTBOL_SPILL_REGS2 : 0));
+// envs_v1's exact squares (glibc pow) as one batch per site with LDS-staged tables (N <= 5), or one
+// body / player at a time with the tables read from global memory (N >= 6: the large instances run at
+// the register limit, where the batches' arrays added spills and the code-generation faults moved in)
+template <int N>
+constexpr bool kSqBatch = N <= 5;
 
 // Diagnostic build only (-DFUTBOL_STAMPS, bench.py --stamps): per-wave s_memtime at phase
 // boundaries, accumulated into st.stamps[wave][slot] (kStampStride slots per wave: 0-10 phases,
@@ -959,32 +964,52 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
     // l > vmax  <=>  s2 > T (T = largest double whose rounded sqrt is <= vmax).  x*x decides every
     // body whose s2 is clearly below T; the exact squares are computed (glibc_pow2_need: only the
     // near-midpoint ones take glibc's path) for the bodies that may clamp, whose scale uses them
-    double vq[2 * S::Nb], vsq[2 * S::Nb];
-    uint64_t vneed = 0;
-    sfor<S::Nb>([&](auto K) {
-        constexpr int k = K;
-        e.vx[k] = e.vx[k] * damping + 0.0 * dt;
-        e.vy[k] = e.vy[k] * damping + 0.0 * dt;
-        vq[2 * k] = e.vx[k];
-        vq[2 * k + 1] = e.vy[k];
-        const double thr = k == S::BALL ? P.clamp2_ball : P.clamp2_player;
-        // |pow - x*x| <= 1 ulp per square: below T (1 - 2^-40) neither s2 exceeds T
-        vneed |= (uint64_t)(e.vx[k] * e.vx[k] + e.vy[k] * e.vy[k] > thr * (1.0 - 0x1.0p-40)) * (3ull << (2 * k));
-    });
-    // (the LDS rows are free here: the narrowphase's staging is consumed, the solve's not yet written)
-    static_assert(sizeof(L.sh->rows) >= (size_t)kPowTabBytes, "pow tables fit the solver rows");
-    glibc_pow2_need_lds<2 * S::Nb>(vq, vsq, vneed, &L.sh->rows[0][0]);
-    sfor<S::Nb>([&](auto K) {
-        constexpr int k = K;
-        const double s2 = vsq[2 * k] + vsq[2 * k + 1];
-        const double thr = k == S::BALL ? P.clamp2_ball : P.clamp2_player;
-        if (((vneed >> (2 * k)) & 1u) && s2 > thr) {
-            constexpr double vmax = k == S::BALL ? kBallVmax : kPlayerVmax;
-            const double sc = vmax / sqrt(s2);
-            e.vx[k] = e.vx[k] * sc;
-            e.vy[k] = e.vy[k] * sc;
-        }
-    });
+    if constexpr (kSqBatch<N>) {
+        double vq[2 * S::Nb], vsq[2 * S::Nb];
+        uint64_t vneed = 0;
+        sfor<S::Nb>([&](auto K) {
+            constexpr int k = K;
+            e.vx[k] = e.vx[k] * damping + 0.0 * dt;
+            e.vy[k] = e.vy[k] * damping + 0.0 * dt;
+            vq[2 * k] = e.vx[k];
+            vq[2 * k + 1] = e.vy[k];
+            const double thr = k == S::BALL ? P.clamp2_ball : P.clamp2_player;
+            // |pow - x*x| <= 1 ulp per square: below T (1 - 2^-40) neither s2 exceeds T
+            vneed |= (uint64_t)(e.vx[k] * e.vx[k] + e.vy[k] * e.vy[k] > thr * (1.0 - 0x1.0p-40)) * (3ull << (2 * k));
+        });
+        // (the LDS rows are free here: the narrowphase's staging is consumed, the solve's not yet written)
+        static_assert(sizeof(L.sh->rows) >= (size_t)kPowTabBytes, "pow tables fit the solver rows");
+        glibc_pow2_need_lds<2 * S::Nb>(vq, vsq, vneed, &L.sh->rows[0][0]);
+        sfor<S::Nb>([&](auto K) {
+            constexpr int k = K;
+            const double s2 = vsq[2 * k] + vsq[2 * k + 1];
+            const double thr = k == S::BALL ? P.clamp2_ball : P.clamp2_player;
+            if (((vneed >> (2 * k)) & 1u) && s2 > thr) {
+                constexpr double vmax = k == S::BALL ? kBallVmax : kPlayerVmax;
+                const double sc = vmax / sqrt(s2);
+                e.vx[k] = e.vx[k] * sc;
+                e.vy[k] = e.vy[k] * sc;
+            }
+        });
+    } else {  // N >= 6: one body at a time, tables from global memory (few live registers)
+        sfor<S::Nb>([&](auto K) {
+            constexpr int k = K;
+            e.vx[k] = e.vx[k] * damping + 0.0 * dt;
+            e.vy[k] = e.vy[k] * damping + 0.0 * dt;
+            const double thr = k == S::BALL ? P.clamp2_ball : P.clamp2_player;
+            const bool near = e.vx[k] * e.vx[k] + e.vy[k] * e.vy[k] > thr * (1.0 - 0x1.0p-40);
+            const double vq[2] = {e.vx[k], e.vy[k]};
+            double vsq[2];
+            glibc_pow2_need<2>(vq, vsq, near ? 3ull : 0ull);
+            const double s2 = vsq[0] + vsq[1];
+            if (near && s2 > thr) {
+                constexpr double vmax = k == S::BALL ? kBallVmax : kPlayerVmax;
+                const double sc = vmax / sqrt(s2);
+                e.vx[k] = e.vx[k] * sc;
+                e.vy[k] = e.vy[k] * sc;
+            }
+        });
+    }
 
     FUTBOL_STAMP(dtc == 2 ? 5 : 9);
     {
@@ -1553,9 +1578,6 @@ __device__ __forceinline__ void do_reset(const V1Params& P, const V1Params* __re
 // players: more lanes with a second passer, more registers), N >= 6 keeps the blocks in the branch
 template <int N>
 constexpr bool kPassDraws = N >= 3 && N <= 5;
-#ifndef FUTBOL_PA_SPLIT  // _process_action's player loop in three passes (v1_step_body)
-#define FUTBOL_PA_SPLIT 0
-#endif
 struct PassDraws {
     uint32_t j0;
     uint32_t a0, b0, a1, b1;  // words 0 and 1 of the blocks at j0 and j0 + 1 (all choice_of reads)
@@ -1573,56 +1595,9 @@ struct PassDraws {
     }
 };
 
-// the teammate index (0..N-1 within the side) chosen by get_pass_target_teammate: the draws only
-template <int N, int side, int me>
-__device__ __forceinline__ int pass_choice(const Env<N>& e, Stream& rs, PassDraws& pd, int ar)
-{
-    constexpr int base = side * N;
-    if constexpr (N == 1) {
-        return 0;
-    } else {
-        int t;
-        if constexpr (N - 1 == 1) {
-            rs.skip(1);
-            t = 0;
-        } else {
-            t = kPassDraws<N> ? pd.choice(rs, N - 1) : rs.choice(N - 1);
-        }
-        t = t >= me ? t + 1 : t;
-        if (ar != 0) {
-            const double x0 = e.px[base + me], y0 = e.py[base + me];
-            auto dir_ok = [&](double mx, double my) {
-                return ((ar == 1) & (my > 0)) | ((ar == 2) & (mx > 0)) | ((ar == 3) & (my < 0)) | ((ar == 4) & (mx < 0));
-            };
-            int cnt = 0;
-            sfor<N>([&](auto Q) {
-                constexpr int q = Q;
-                cnt += dir_ok(e.px[base + q] - x0, e.py[base + q] - y0) ? 1 : 0;
-            });
-            if (cnt > 0) {
-                int pick;
-                if constexpr (N - 1 == 1) {
-                    rs.skip(1);
-                    pick = 0;
-                } else {
-                    pick = kPassDraws<N> ? pd.choice(rs, cnt) : rs.choice(cnt);
-                }
-                sfor<N>([&](auto Q) {
-                    constexpr int q = Q;
-                    if (dir_ok(e.px[base + q] - x0, e.py[base + q] - y0)) {
-                        if (pick == 0) t = q;
-                        --pick;
-                    }
-                });
-            }
-        }
-        return t;
-    }
-}
-
-template <int N, int side, int me>
+template <int N, int side, int me, int NSQ>
 __device__ __forceinline__ void pass_target(const Env<N>& e, Stream& rs, PassDraws& pd, int ar, double& tx, double& ty,
-                                            const double (&sq)[4 * N + 3], double& sx, double& sy)
+                                            const double (&sq)[NSQ], double& sx, double& sy)
 {
     constexpr int base = side * N;
     if constexpr (N == 1) {
@@ -1681,8 +1656,10 @@ __device__ __forceinline__ void pass_target(const Env<N>& e, Stream& rs, PassDra
             const double sel = q == t ? 1.0 : 0.0;
             tx = __builtin_fma(sel, e.px[base + q], tx);
             ty = __builtin_fma(sel, e.py[base + q], ty);
-            sx = __builtin_fma(sel, sq[2 * (base + q)], sx);  // the target's squares (ball - teammate)^2
-            sy = __builtin_fma(sel, sq[2 * (base + q) + 1], sy);
+            if constexpr (kSqBatch<N>) {
+                sx = __builtin_fma(sel, sq[2 * (base + q)], sx);  // the target's squares (ball - teammate)^2
+                sy = __builtin_fma(sel, sq[2 * (base + q) + 1], sy);
+            }
         });
     }
 }
@@ -1823,10 +1800,10 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
     // do not change in the loop, so every candidate d is known now -- ball - player k (press; a
     // pass to teammate k squares k - ball, the same squares) and goal - ball (shoot) -- and their
     // exact squares are one batch: the near-midpoint ones of the squares some lane may use
-    constexpr int NSQ = 4 * N + 3;
+    constexpr int NSQ = kSqBatch<N> ? 4 * N + 3 : 1;  // (N >= 6: per player, in the loop below)
     double sqin[NSQ], sq[NSQ];
     uint64_t sqneed = 0;
-    {
+    if constexpr (kSqBatch<N>) {
         uint32_t pass_side = 0, shoot_side = 0;
         sfor<2 * N>([&](auto K) {
             constexpr int k = K;
@@ -1848,94 +1825,8 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
         sqneed |= ((uint64_t)(shoot_side & 1u) << (4 * N)) | ((uint64_t)(shoot_side >> 1) << (4 * N + 1)) |
                   ((uint64_t)(shoot_side != 0) << (4 * N + 2));
     }
-    glibc_pow2_need_lds<NSQ>(sqin, sq, sqneed, &sh.rows[0][0]);  // (rows: unused until space_step)
-#if FUTBOL_PA_SPLIT
-    // The loop in three passes, same arithmetic and draw order: only the ball's velocity (dribble,
-    // kick) and the owner carry from one player to the next -- a player's own velocity, its direction
-    // d and the quotients S * d / |d| depend on the positions alone.  (A) the pass targets, in player
-    // order (their draws, with the divergent branches of the N >= 3 choice); (B) every player's sqrt and
-    // two divisions and its own velocity, in one basic block, so that the scheduler overlaps the 2N
-    // independent quotient chains; (C) the ball's velocity chain and the owner, in player order.
-    int tgt[2 * N];
-    sfor<2 * N>([&](auto K) {
-        constexpr int k = K;
-        constexpr int side = k < N ? 0 : 1;
-        const int ar = arrow[k];
-        const bool pass = (key[k] == 4) & touch[k];
-        if constexpr (N == 2) {
-            constexpr int mate = side * N + (1 - (k - side * N));
-            const double mx = e.px[mate] - e.px[k], my = e.py[mate] - e.py[k];
-            const bool way = ((ar == 1) & (my > 0)) | ((ar == 2) & (mx > 0)) | ((ar == 3) & (my < 0)) | ((ar == 4) & (mx < 0));
-            rs.skip(pass ? (way ? 2u : 1u) : 0u);
-            tgt[k] = mate - side * N;
-        } else {
-            tgt[k] = 0;
-            if (pass) tgt[k] = pass_choice<N, side, k - side * N>(e, rs, pd, ar);
-        }
-    });
-    double fdxa[2 * N], fdya[2 * N];
-    sfor<2 * N>([&](auto K) {
-        constexpr int k = K;
-        constexpr int side = k < N ? 0 : 1;
-        constexpr int base = side * N;
-        const int ar = arrow[k], ky = key[k];
-        const bool tk = touch[k];
-        const int fx = ar == 2 ? 1 : (ar == 4 ? -1 : 0);
-        const int fy = ar == 1 ? 1 : (ar == 3 ? -1 : 0);
-        const bool move = ky <= 1;
-        const bool shoot = (ky == 2) & tk;
-        const bool press = (ky == 3) & !tk & (ar == 0);
-        double tx, ty, tsx, tsy;  // the pass target's position and squares (exact selects, see pass_target)
-        if constexpr (N == 2) {
-            constexpr int mate = side * N + (1 - (k - side * N));
-            tx = e.px[mate];
-            ty = e.py[mate];
-            tsx = sq[2 * mate];
-            tsy = sq[2 * mate + 1];
-        } else {
-            tx = 0.0;
-            ty = 0.0;
-            tsx = 0.0;
-            tsy = 0.0;
-            sfor<N>([&](auto Q) {
-                constexpr int q = Q;
-                const double sel = q == tgt[k] ? 1.0 : 0.0;
-                tx = __builtin_fma(sel, e.px[base + q], tx);
-                ty = __builtin_fma(sel, e.py[base + q], ty);
-                tsx = __builtin_fma(sel, sq[2 * (base + q)], tsx);
-                tsy = __builtin_fma(sel, sq[2 * (base + q) + 1], tsy);
-            });
-        }
-        const double gx = side == 0 ? W : 0.0, gy = H / 2;
-        const double ox = press ? e.px[k] : e.px[BL], oy = press ? e.py[k] : e.py[BL];
-        const double qx = press ? e.px[BL] : (shoot ? gx : tx), qy = press ? e.py[BL] : (shoot ? gy : ty);
-        const double dx = qx - ox, dy = qy - oy;
-        const double sx = press ? sq[2 * k] : (shoot ? sq[4 * N + side] : tsx);
-        const double sy = press ? sq[2 * k + 1] : (shoot ? sq[4 * N + 2] : tsy);
-        const double mag = sqrt(sx + sy);
-        const double S = press ? 40.0 : (shoot ? 120.0 : 100.0);
-        fdxa[k] = S * dx / mag;
-        fdya[k] = S * dy / mag;
-        const int f = ky == 0 ? 20 : 40;
-        const double mvx = e.vx[k] + (double)(f * fx) * kPlayerMinv, mvy = e.vy[k] + (double)(f * fy) * kPlayerMinv;
-        const double pvx = e.vx[k] + fdxa[k] * kPlayerMinv, pvy = e.vy[k] + fdya[k] * kPlayerMinv;
-        e.vx[k] = move ? mvx : (press ? pvx : e.vx[k]);
-        e.vy[k] = move ? mvy : (press ? pvy : e.vy[k]);
-    });
-    sfor<2 * N>([&](auto K) {
-        constexpr int k = K;
-        constexpr int side = k < N ? 0 : 1;
-        const int ky = key[k];
-        const bool tk = touch[k];
-        const bool move = ky <= 1, shoot = (ky == 2) & tk, pass = (ky == 4) & tk;
-        const double D = shoot ? 2.0 : 10.0, rD = shoot ? 0.5 : 0.1;
-        const double kvx = cdiv(e.vx[BL], D, rD) + fdxa[k] * kBallMinv, kvy = cdiv(e.vy[BL], D, rD) + fdya[k] * kBallMinv;
-        const bool dribble = move & tk, kick = shoot | pass;
-        e.vx[BL] = dribble ? e.vx[k] : (kick ? kvx : e.vx[BL]);
-        e.vy[BL] = dribble ? e.vy[k] : (kick ? kvy : e.vy[BL]);
-        owner = tk ? (uint32_t)side : owner;
-    });
-#else
+    if constexpr (kSqBatch<N>)
+        glibc_pow2_need_lds<NSQ>(sqin, sq, sqneed, &sh.rows[0][0]);  // (rows: unused until space_step)
     sfor<2 * N>([&](auto K) {
         constexpr int k = K;
         constexpr int side = k < N ? 0 : 1;
@@ -1972,8 +1863,19 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
         const double ox = press ? e.px[k] : e.px[BL], oy = press ? e.py[k] : e.py[BL];
         const double qx = press ? e.px[BL] : (shoot ? gx : tx), qy = press ? e.py[BL] : (shoot ? gy : ty);
         const double dx = qx - ox, dy = qy - oy;
-        const double sx = press ? sq[2 * k] : (shoot ? sq[4 * N + side] : tsx);
-        const double sy = press ? sq[2 * k + 1] : (shoot ? sq[4 * N + 2] : tsy);
+        double sx, sy;
+        if constexpr (kSqBatch<N>) {
+            sx = press ? sq[2 * k] : (shoot ? sq[4 * N + side] : tsx);
+            sy = press ? sq[2 * k + 1] : (shoot ? sq[4 * N + 2] : tsy);
+        } else {  // N >= 6: this player's two squares (tables from global memory)
+            const double q2[2] = {dx, dy};
+            double s2[2];
+            glibc_pow2_need<2>(q2, s2, (press | shoot | pass) ? 3ull : 0ull);
+            sx = s2[0];
+            sy = s2[1];
+            (void)tsx;
+            (void)tsy;
+        }
         const double mag = sqrt(sx + sy);
         const double S = press ? 40.0 : (shoot ? 120.0 : 100.0);
         const double fdx = S * dx / mag, fdy = S * dy / mag;
@@ -1991,7 +1893,6 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
         e.vy[BL] = dribble ? e.vy[k] : (kick ? kvy : e.vy[BL]);
         owner = tk ? (uint32_t)side : owner;
     });
-#endif
 
     // check_and_fix_out_bounds (:247-287), before physics
     bool out = false;
