@@ -394,6 +394,8 @@ def main():
     ap.add_argument("--kind", default="v1", choices=["v1", "v0", "c1"],
                     help="v1: envs_v1 (C2/C4, --players 5: C5); v0: hard-coded opponent (C3); c1: the C1 CPU line")
     ap.add_argument("--graph", type=int, default=1, help="replay the timed steps from a hipGraph")
+    ap.add_argument("--direct", type=int, default=0,
+                    help="1: launch the timed steps one by one (pre-generated actions, no hipGraph)")
     ap.add_argument("--groups", type=int, default=1,
                     help="step the B envs as this many independent env groups (B/groups envs each: one "
                          "context, HIP stream and hipGraph per group) that advance asynchronously")
@@ -574,6 +576,10 @@ def main():
         stream.wait_stream(s)
         return g_
 
+    direct_abuf = None
+    if args.direct:  # the timed steps launched one by one from Python, actions pre-generated like the graphs'
+        args.graph = 0
+        direct_abuf = torch.zeros((args.steps, venv.num_envs, venv.action_dim), dtype=torch.uint8, device=dev)
     if args.graph:
         graphs = []
         for ge, s in zip(groups, streams):
@@ -623,6 +629,9 @@ def main():
     for ge in groups:
         ge.episode_stats(clear=True)
     fill_ms = None
+    if direct_abuf is not None:
+        venv.random_actions_steps(args.steps, ALL, seed=1234, out=direct_abuf)
+        torch.cuda.synchronize(dev)
     if graphs is not None:  # the synthetic inputs of the K timed steps, fresh draws, into HBM
         f0, f1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         f0.record(stream)
@@ -636,10 +645,10 @@ def main():
         fill_ms = f0.elapsed_time(f1) / args.steps
     D.barrier(dev)
     torch.cuda.synchronize(dev)
-    dbg = os.environ.get("FUTBOL_BENCH_DEBUG") and graphs is not None
+    dbg = os.environ.get("FUTBOL_BENCH_DEBUG") and (graphs is not None or direct_abuf is not None)
     if dbg:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ev0.record(streams[0])
+        ev0.record(streams[0] if graphs is not None else stream)
     t0 = time.perf_counter()
     done_steps = 0
     ci = 0
@@ -656,6 +665,8 @@ def main():
                     for _ in range(chunk):
                         ge.random_actions(ALL, seed=1234, out=ge._act)
                         ge.step_raw(ge._act)
+        elif direct_abuf is not None:
+            venv.step_raw(direct_abuf[done_steps])
         else:
             for _ in range(chunk):
                 one_step()
@@ -667,7 +678,7 @@ def main():
             stats_buf.copy_(all_stats())
             D.reduce_episode_stats(stats_buf)  # RCCL over xGMI: [sum return, episodes, env-steps]
     if dbg:
-        ev1.record(streams[0])
+        ev1.record(streams[0] if graphs is not None else stream)
     torch.cuda.synchronize(dev)
     D.barrier(dev)
     elapsed = D.max_over_ranks(time.perf_counter() - t0, dev)
@@ -693,11 +704,13 @@ def main():
                    "actions": ("synthetic Philox left-team actions of all %d timed steps drawn on the GPU by one "
                                "fill launch before the timed region (resident in HBM, not timed; the fill costs "
                                "action_fill_ms_per_step); the opponent's actions are drawn inside the step kernel"
-                               % args.steps) if graphs is not None else
+                               % args.steps) if (graphs is not None or direct_abuf is not None) else
                               "synthetic Philox left-team actions drawn by a fill launch before every step (timed)",
                    "action_fill_ms_per_step": fill_ms,
                    "launch": ("open-loop rollout launches of up to %d steps (futbol_rollout; every step writes its "
-                              "obs / reward / done slice)" % RL) if RL else "one futbol_step launch per step",
+                              "obs / reward / done slice)" % RL) if RL else
+                             ("one futbol_step launch per step, launched one by one" if direct_abuf is not None else
+                              "one futbol_step launch per step, replayed from hipGraphs"),
                    "episode_phases": "staggered" if args.stagger else "lockstep (DummyVecEnv)",
                    "timed_from_episode_step": None if args.stagger else
                    (args.warmup + 2 * args.profile_steps + (args.steps if graphs is not None else 0) + align)

@@ -26,14 +26,6 @@ ARCH = os.environ.get("FUTBOL_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fPIC",
           "-Wall", "-Wno-unused-function", "-I" + os.path.join(ROOT, "include")]
-# No pre-RA exec-mask optimization (SIOptimizeExecMaskingPreRA).  With it, the register allocator's
-# live-range-split copies (v_accvgpr_write aN, vM ...) of values live in every lane ended up at the
-# top of a join block BEFORE its exec restore -- executed with the inner branch's lanes only, or none
-# -- in the step instances at high register pressure: the cause of round 3's wrong results and
-# illegal address ("compiler").  scripts/isa_exec_check.py / tests/test_isa_exec.py
-# check every built kernel for the pattern.  FUTBOL_EXEC_OPT_PRE_RA=1 restores LLVM's default.
-if os.environ.get("FUTBOL_EXEC_OPT_PRE_RA", "0") != "1":
-    CFLAGS += ["-mllvm", "-amdgpu-opt-exec-mask-pre-ra=false"]
 # SimplifyCFG folds an if/else whose arms cost up to this many instructions into selects: the
 # default (4) leaves the fp64 arms of the action / contact code as divergent branches (~40 cycles
 # each on a wave64); 20 measured best for the 2v2 step (-1.5% step time).  Only for the N <= 3
@@ -125,7 +117,12 @@ def _stale(target, sources):
 # recompiled with the next of these register-allocation / scheduling variants (each changes where the
 # allocator splits live ranges) until none is found; the build fails if every variant has findings.
 # The variant used is recorded in the object's stamp.  FUTBOL_ISA_GATE=0 skips the gate.
-GATE_VARIANTS = [[], ["-mllvm", "-split-spill-mode=size"], ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+# The first fallback switches LLVM's pre-RA exec-mask optimization (SIOptimizeExecMaskingPreRA) off: with
+# it, the copies of the N = 7 segment-candidate loop's exit landed before the restore.  (Off for every TU,
+# the kernels measured 1-2% slower: 2v2 22.66 vs 22.42 us, v0 22.92 vs 22.45 us, 5v5 52.8 vs 52.3 us.)
+NO_PRE_RA = ["-mllvm", "-amdgpu-opt-exec-mask-pre-ra=false"]
+GATE_VARIANTS = [[], NO_PRE_RA, ["-mllvm", "-split-spill-mode=size"], ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+                 NO_PRE_RA + ["-mllvm", "-split-spill-mode=size"], NO_PRE_RA + ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
                  ["-mllvm", "-split-spill-mode=size", "-mllvm", "-amdgpu-sched-strategy=max-ilp"]]
 GATE = os.environ.get("FUTBOL_ISA_GATE", "1") != "0"
 

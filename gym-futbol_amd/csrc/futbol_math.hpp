@@ -529,10 +529,9 @@ __device__ __forceinline__ void glibc_pow2_need_lds(const double (&x)[M], double
             for (int i = 0; i < M; ++i) h[i] = bit == (1ull << i) ? f : h[i];
             pend &= pend - 1u;
         }
-        // The caller reuses this LDS with other types next (the solver rows are double2): without a
-        // barrier here, type-based alias analysis may move those stores above the last u64 / double
-        // table reads (it did: the N = 6 f64 runtime-geometry rollout instance read positions as
-        // exp-table entries from step 18 on, with LLVM's default scheduler)
+        // The caller reuses this LDS with other types next (the solver rows are double2): the barrier
+        // keeps those stores after the last u64 / double table reads whatever type-based alias analysis
+        // concludes (a precaution: it was not the cause of the N = 6 divergence)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
