@@ -79,6 +79,8 @@ int futbol_config_default(int32_t env_kind, int32_t number_of_player, FutbolConf
    Runs each env's constructor (which in the reference already calls reset()). */
 int futbol_create(const FutbolConfig* cfg, int32_t device, uint64_t seed, uint64_t env_id_base,
                   int32_t num_envs, FutbolCtx** out);
+/* Releases every resource of ctx (NULL: no-op) whatever fails; returns FUTBOL_EHIP if a HIP call
+   failed, with its text in futbol_last_error(NULL) (the context is gone). */
 int futbol_destroy(FutbolCtx* ctx);
 const char* futbol_last_error(const FutbolCtx* ctx);
 
