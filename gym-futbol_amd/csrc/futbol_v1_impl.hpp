@@ -61,9 +61,13 @@ constexpr double kE = 0.2;  // elasticity of players and ball; segments 0
 #endif
 template <int N>
 constexpr int CKN = N >= 6 ? FUTBOL_CK_BIG : (N >= 5 ? FUTBOL_CK_LARGE : FUTBOL_CK_SMALL);
-// entries beyond CKN read per batch of independent loads (5v5 and up: registers are exhausted)
+// entries beyond CKN read per batch of independent loads: each batch is one memory round trip on
+// the lane's lookup and filter loops (10v10 189 -> 174 us with 4 instead of 1; 5v5 neutral)
+#ifndef FUTBOL_CBN_LARGE
+#define FUTBOL_CBN_LARGE 4
+#endif
 template <int N>
-constexpr int CBN = N >= 5 ? 1 : 4;
+constexpr int CBN = N >= 5 ? FUTBOL_CBN_LARGE : 4;
 // spill records (slots past the LDS ones) an item of the split solve holds in registers for its
 // 10 sweeps: read from the global spill area once, written back once.  The 5v5 instance spills on
 // 13% of its waves (4 measured best: 2 / 6 slower), 10v10 (2 LDS slots) on most (2 best, 4 neutral);
@@ -156,6 +160,18 @@ constexpr bool kSolveComponents = 2 * N + 1 <= 8;
 #ifndef FUTBOL_K5
 #define FUTBOL_K5 4
 #endif
+// N = 8..10 (one set of solver rows): as many slots as keep a block within 40 KB (4 blocks per CU);
+// records past the slots are re-read from the global spill area in every sweep (10v10: 2 -> 4 slots,
+// 175 -> 166 us)
+#ifndef FUTBOL_K8
+#define FUTBOL_K8 5
+#endif
+#ifndef FUTBOL_K9
+#define FUTBOL_K9 4
+#endif
+#ifndef FUTBOL_K10
+#define FUTBOL_K10 4
+#endif
 // One set of solver rows (N >= FUTBOL_ONE_ROWS_MIN, round 4): the LDS holds Nb + 1 rows per lane
 // instead of 2 Nb + 1 -- the narrowphase stages positions, then velocities, in the same rows (each
 // record's bounce is a second pass over the contact work list), and the split solve runs the v half
@@ -173,10 +189,10 @@ struct V1Shape {
     static constexpr bool ONE_ROWS = N >= FUTBOL_ONE_ROWS_MIN;
     static constexpr int NROWS = ONE_ROWS ? Nb + 1 : 2 * Nb + 1;
     // LDS contact-record slots per lane: 4 one-wave blocks per CU must fit in 160 KB
-    // (40 KB per block: K * 4 KB of records + (2 Nb + 1) KB of solver velocity rows + the segment table)
-    // for N <= 7; N = 8, 9, 10 (the rows alone take 35-43 KB) fit 3 blocks per CU (53 KB each)
+    // (40 KB per block: K * 4 KB of records + (2 Nb + 1) KB of solver velocity rows + the segment table;
+    // N = 8..10: Nb + 1 KB of rows, ONE_ROWS)
     static constexpr int K = N == 1 ? 8 : (N == 2 ? FUTBOL_K2 : (N == 3 ? 6 : (N == 4 ? 5 : (N == 5 ? FUTBOL_K5 :
-                             (N == 6 ? 3 : (N == 7 ? 2 : (N == 8 ? 4 : (N == 9 ? 3 : 2))))))));
+                             (N == 6 ? 3 : (N == 7 ? 2 : (N == 8 ? FUTBOL_K8 : (N == 9 ? FUTBOL_K9 : FUTBOL_K10))))))));
 };
 
 __device__ __forceinline__ double minv_of(int k, int ball) { return k == ball ? kBallMinv : kPlayerMinv; }

@@ -318,3 +318,46 @@ def test_rollout_rejects_bad_out_buffers():
             env.rollout(acts, out=out)
     env.rollout(acts, out=good)  # the right buffers are accepted
     env.close()
+
+
+@pytest.mark.parametrize("env_id,B,dtype", [("Futbol2v2-v1", 99, torch.float32), ("Futbol2v2-v1", 99, torch.float64),
+                                            ("Futbol-v1", 77, torch.float32), ("Futbol-v1", 77, torch.float64),
+                                            ("Futbol-v0", 99, torch.float32), ("Futbol-v0", 101, torch.float64)])
+def test_obs_store_alignment_and_ragged_blocks(env_id, B, dtype):
+    """The C ABI takes any element-aligned device buffer: an observation buffer one element off
+    16-byte alignment, with guard elements on both sides, gets the same observations bit for bit as
+    an allocation of its own and nothing outside its rows, for the ragged last block of each kind
+    and both output dtypes (futbol_rollout and futbol_step)."""
+    K = 320  # through an episode end
+    a = gf.make(env_id, num_envs=B, seed=8, dtype=dtype)
+    b = gf.make(env_id, num_envs=B, seed=8, dtype=dtype)
+    a.reset()
+    b.reset()
+    acts = a.random_actions_steps(K, 0, seed=3)
+    ref = a.rollout(acts)
+    od = int(np.prod(a.obs_shape))
+    n = K * B * od
+    flat = torch.full((n + 3,), 7.25, dtype=dtype, device=a.device)
+    obs = flat[1:1 + n].view((K, B) + tuple(a.obs_shape))
+    assert obs.data_ptr() % 16 != 0
+    out = (obs, torch.empty_like(ref[1]), torch.empty_like(ref[2]), torch.empty_like(ref[3]))
+    b.rollout(acts, out=out)
+    assert torch.equal(obs, ref[0]) and torch.equal(out[1], ref[1]) and torch.equal(out[2], ref[2])
+    assert flat[0].item() == 7.25 and flat[-2:].eq(7.25).all()
+    # single steps into an unaligned buffer too (futbol_step's own instance)
+    a.reset()
+    b.reset()
+    for k in range(3):
+        o, _, _, _ = a.step(acts[k])
+        o_ref = o.clone()
+        ob = flat[1:1 + B * od].view((B,) + tuple(a.obs_shape))
+        rb = torch.empty(B, dtype=dtype, device=a.device)
+        db = torch.empty(B, dtype=torch.uint8, device=a.device)
+        with torch.cuda.device(b.device):
+            gf._native.check(gf._native.load().futbol_step(b.ctx.h, acts[k].data_ptr(), ob.data_ptr(), rb.data_ptr(),
+                                                          db.data_ptr(), None, torch.cuda.current_stream().cuda_stream),
+                             b.ctx.h)
+        torch.cuda.synchronize()
+        assert torch.equal(ob, o_ref), k
+    a.close()
+    b.close()
