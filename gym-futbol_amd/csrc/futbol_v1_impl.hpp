@@ -62,9 +62,10 @@ constexpr double kE = 0.2;  // elasticity of players and ball; segments 0
 template <int N>
 constexpr int CKN = N >= 6 ? FUTBOL_CK_BIG : (N >= 5 ? FUTBOL_CK_LARGE : FUTBOL_CK_SMALL);
 // entries beyond CKN read per batch of independent loads: each batch is one memory round trip on
-// the lane's lookup and filter loops (10v10 189 -> 174 us with 4 instead of 1; 5v5 neutral)
+// the lane's lookup and filter loops (10v10 189 -> 174 us with 4 instead of 1, -2% more with 8;
+// 5v5 neutral)
 #ifndef FUTBOL_CBN_LARGE
-#define FUTBOL_CBN_LARGE 4
+#define FUTBOL_CBN_LARGE 8
 #endif
 template <int N>
 constexpr int CBN = N >= 5 ? FUTBOL_CBN_LARGE : 4;
@@ -75,8 +76,8 @@ constexpr int CBN = N >= 5 ? FUTBOL_CBN_LARGE : 4;
 #ifndef FUTBOL_SPILL_REGS
 #define FUTBOL_SPILL_REGS 4
 #endif
-#ifndef FUTBOL_SPILL_REGS_BIG  // N >= 6 (10v10 measured 2 best in round 2; 0 now, for register pressure)
-#define FUTBOL_SPILL_REGS_BIG 0
+#ifndef FUTBOL_SPILL_REGS_BIG  // N >= 6 (10v10 with 4 LDS slots: 0 -> 2 -> 4, 166 -> 161.5 -> 158.8 us)
+#define FUTBOL_SPILL_REGS_BIG 4
 #endif
 #ifndef FUTBOL_SPILL_REGS2
 #define FUTBOL_SPILL_REGS2 0
@@ -1487,17 +1488,40 @@ __device__ __forceinline__ void write_obs(const Env<N>& e, OT* o)
     });
 }
 
+// The step kernel's v_bias loads for N >= FUTBOL_LATE_BIAS_MIN: issued after the action phase (the
+// first use is the position update) instead of with the rest of the state, so that 2 Nb doubles are
+// not live through _process_action's player loop at the register limit
+// (10v10: 158.8 -> 146.3 us)
+#ifndef FUTBOL_LATE_BIAS_MIN
+#define FUTBOL_LATE_BIAS_MIN 6
+#endif
 template <int N>
+constexpr bool kLateBias = N >= FUTBOL_LATE_BIAS_MIN;
+
+template <int N, bool BIAS = true>
 __device__ __forceinline__ void load_bodies(const V1Ptrs& st, int env, int B, Env<N>& e)
 {
     sfor<V1Shape<N>::Nb>([&](auto K) {
         constexpr int k = K;
         const size_t o = (size_t)k * B + env;
-        const double2 p = st.pxy[o], v = st.vxy[o], vb = st.bxy[o];
+        const double2 p = st.pxy[o], v = st.vxy[o];
         e.px[k] = p.x;
         e.py[k] = p.y;
         e.vx[k] = v.x;
         e.vy[k] = v.y;
+        if constexpr (BIAS) {
+            const double2 vb = st.bxy[o];
+            e.bx[k] = vb.x;
+            e.by[k] = vb.y;
+        }
+    });
+}
+template <int N>
+__device__ __forceinline__ void load_bias(const V1Ptrs& st, int env, int B, Env<N>& e)
+{
+    sfor<V1Shape<N>::Nb>([&](auto K) {
+        constexpr int k = K;
+        const double2 vb = st.bxy[(size_t)k * B + env];
         e.bx[k] = vb.x;
         e.by[k] = vb.y;
     });
@@ -1735,7 +1759,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
     }
     Env<N> e;
     e.meta.w = st.meta[env];
-    load_bodies<N>(st, env, B, e);
+    load_bodies<N, !kLateBias<N>>(st, env, B, e);
     uint32_t ck[CKN<N>];
     double cj[CKN<N>];
     load_cache_pre<N, EPW>(L, e.meta.ncache(), ck, cj);
@@ -1947,6 +1971,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
     // the segment table's loads were issued with the state's; every lane of the block is here
     store_seg<N, EPW>(seg_g, sh);
     if (!live) return;
+    if constexpr (kLateBias<N>) load_bias<N>(st, env, B, e);
     FUTBOL_CRUMB(L, 3);
     FUTBOL_STAMP(2);
 
