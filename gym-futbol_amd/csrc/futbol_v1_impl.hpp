@@ -1490,13 +1490,19 @@ __device__ __forceinline__ void write_obs(const Env<N>& e, OT* o)
 
 // The step kernel's v_bias loads for N >= FUTBOL_LATE_BIAS_MIN: issued after the action phase (the
 // first use is the position update) instead of with the rest of the state, so that 2 Nb doubles are
-// not live through _process_action's player loop at the register limit
-// (10v10: 158.8 -> 146.3 us)
+// not live through _process_action's player loop at the register limit (one more memory round trip)
+// (10v10: 158.8 -> 146.3 us, 5v5: 53.0 -> 51.8 us; 2v2 has no spills to save)
 #ifndef FUTBOL_LATE_BIAS_MIN
-#define FUTBOL_LATE_BIAS_MIN 6
+#define FUTBOL_LATE_BIAS_MIN 5
 #endif
 template <int N>
 constexpr bool kLateBias = N >= FUTBOL_LATE_BIAS_MIN;
+// likewise the preloaded arbiter-cache entries (first used after the narrowphase's hit tests)
+#ifndef FUTBOL_LATE_CACHE_MIN
+#define FUTBOL_LATE_CACHE_MIN 99
+#endif
+template <int N>
+constexpr bool kLateCache = N >= FUTBOL_LATE_CACHE_MIN;
 
 template <int N, bool BIAS = true>
 __device__ __forceinline__ void load_bodies(const V1Ptrs& st, int env, int B, Env<N>& e)
@@ -1762,7 +1768,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
     load_bodies<N, !kLateBias<N>>(st, env, B, e);
     uint32_t ck[CKN<N>];
     double cj[CKN<N>];
-    load_cache_pre<N, EPW>(L, e.meta.ncache(), ck, cj);
+    if constexpr (!kLateCache<N>) load_cache_pre<N, EPW>(L, e.meta.ncache(), ck, cj);
     const double ep_ret0 = st.ep_ret[env];
     // lanes past B (last block) run the action phase on their shadow copy of env B-1 in
     // registers only (no store, no counter) and leave after the segment table is in LDS
@@ -1972,6 +1978,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
     store_seg<N, EPW>(seg_g, sh);
     if (!live) return;
     if constexpr (kLateBias<N>) load_bias<N>(st, env, B, e);
+    if constexpr (kLateCache<N>) load_cache_pre<N, EPW>(L, e.meta.ncache(), ck, cj);  // (first use: the cache lookups)
     FUTBOL_CRUMB(L, 3);
     FUTBOL_STAMP(2);
 
