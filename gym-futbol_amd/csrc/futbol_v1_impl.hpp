@@ -1497,12 +1497,6 @@ __device__ __forceinline__ void write_obs(const Env<N>& e, OT* o)
 #endif
 template <int N>
 constexpr bool kLateBias = N >= FUTBOL_LATE_BIAS_MIN;
-// likewise the preloaded arbiter-cache entries (first used after the narrowphase's hit tests)
-#ifndef FUTBOL_LATE_CACHE_MIN
-#define FUTBOL_LATE_CACHE_MIN 99
-#endif
-template <int N>
-constexpr bool kLateCache = N >= FUTBOL_LATE_CACHE_MIN;
 
 template <int N, bool BIAS = true>
 __device__ __forceinline__ void load_bodies(const V1Ptrs& st, int env, int B, Env<N>& e)
@@ -1768,7 +1762,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
     load_bodies<N, !kLateBias<N>>(st, env, B, e);
     uint32_t ck[CKN<N>];
     double cj[CKN<N>];
-    if constexpr (!kLateCache<N>) load_cache_pre<N, EPW>(L, e.meta.ncache(), ck, cj);
+    load_cache_pre<N, EPW>(L, e.meta.ncache(), ck, cj);
     const double ep_ret0 = st.ep_ret[env];
     // lanes past B (last block) run the action phase on their shadow copy of env B-1 in
     // registers only (no store, no counter) and leave after the segment table is in LDS
@@ -1978,7 +1972,6 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
     store_seg<N, EPW>(seg_g, sh);
     if (!live) return;
     if constexpr (kLateBias<N>) load_bias<N>(st, env, B, e);
-    if constexpr (kLateCache<N>) load_cache_pre<N, EPW>(L, e.meta.ncache(), ck, cj);  // (first use: the cache lookups)
     FUTBOL_CRUMB(L, 3);
     FUTBOL_STAMP(2);
 
