@@ -419,6 +419,8 @@ def main():
     ap.add_argument("--launcher-selftest", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--launcher-selftest-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.direct and args.rollout:
+        ap.error("--direct launches one futbol_step per step; it cannot be combined with --rollout")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # one process per GPU, started here (nothing has touched the GPU yet); under torchrun the
         # ranks already exist and WORLD_SIZE is set

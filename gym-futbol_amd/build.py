@@ -9,6 +9,7 @@ math must round exactly like the reference's (no FMA contraction).
 """
 import argparse
 import glob
+import json
 import os
 import subprocess
 import sys
@@ -91,11 +92,13 @@ def _sched_flags(src):
     return ["-mllvm", "-amdgpu-sched-strategy=" + SCHED]
 # A/B of compiler options: FUTBOL_EXTRA_CFLAGS="..." (with a FUTBOL_BUILD_VARIANT name)
 CFLAGS += os.environ.get("FUTBOL_EXTRA_CFLAGS", "").split()
-if VARIANT == "stamps":
+# (a variant name's "_"-separated words select these, e.g. FUTBOL_BUILD_VARIANT=kx6_bounds)
+_VWORDS = set(VARIANT.split("_"))
+if "stamps" in _VWORDS:
     CFLAGS.append("-DFUTBOL_STAMPS")
-if VARIANT == "crumbs":  # diagnostic: per-wave phase markers in host-coherent memory
+if "crumbs" in _VWORDS:  # diagnostic: per-wave phase markers in host-coherent memory
     CFLAGS.append("-DFUTBOL_CRUMBS")
-if VARIANT == "bounds":  # diagnostic: index checks that flag and clamp instead of faulting
+if "bounds" in _VWORDS:  # diagnostic: index checks that flag and clamp instead of faulting
     CFLAGS.append("-DFUTBOL_BOUNDS")
 
 
@@ -113,7 +116,9 @@ def _stale(target, sources):
 
 # Code-generation gate ("compiler"): after compiling a TU, its code object is
 # scanned for register copies placed before a join block's exec restore (scripts/isa_exec_check.py),
-# the pattern behind round 3's wrong-result / illegal-address instances.  A TU with a finding is
+# the pattern behind round 3's wrong-result / illegal-address instances, and (round 5) for loaded or
+# computed values that are only copied into registers nobody reads (scripts/isa_liveness.py), the
+# pattern behind round 4's two wrong-result builds.  A TU with a finding is
 # recompiled with the next of these register-allocation / scheduling variants (each changes where the
 # allocator splits live ranges) until none is found; the build fails if every variant has findings.
 # The variant used is recorded in the object's stamp.  FUTBOL_ISA_GATE=0 skips the gate.
@@ -125,12 +130,25 @@ GATE_VARIANTS = [[], NO_PRE_RA, ["-mllvm", "-split-spill-mode=size"], ["-mllvm",
                  NO_PRE_RA + ["-mllvm", "-split-spill-mode=size"], NO_PRE_RA + ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
                  ["-mllvm", "-split-spill-mode=size", "-mllvm", "-amdgpu-sched-strategy=max-ilp"]]
 GATE = os.environ.get("FUTBOL_ISA_GATE", "1") != "0"
+# the lane-aware liveness check (scripts/isa_liveness.py, round 5): FUTBOL_LIVENESS_GATE=0 skips it
+LIVENESS_GATE = os.environ.get("FUTBOL_LIVENESS_GATE", "1") != "0"
 
 
 def _isa_findings(obj):
+    """both static checks of a compiled TU: register copies before an exec restore (isa_exec_check) and
+    values that are only copied to registers nobody reads (isa_liveness: lane-aware liveness, run in a
+    child process so that the TUs' checks run in parallel)"""
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
     import isa_exec_check
-    return isa_exec_check.check_object(obj)
+    found = isa_exec_check.check_object(obj, ARCH)
+    if LIVENESS_GATE:
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "isa_liveness.py"), "--json",
+                            "--arch=" + ARCH, obj], capture_output=True, text=True)
+        if r.returncode not in (0, 1):
+            raise RuntimeError("isa_liveness failed on %s:\n%s" % (obj, r.stderr[-4000:]))
+        for ln in r.stdout.splitlines():
+            found += [(k, a, ["lost value: " + t]) for k, a, t in json.loads(ln)["findings"]]
+    return found
 
 
 def _compile(src, force):
@@ -164,7 +182,7 @@ def _compile(src, force):
                 print("isa gate: %s built with %s" % (os.path.basename(src), " ".join(extra)), flush=True)
             return obj
     os.remove(obj)
-    raise RuntimeError("isa gate: every variant of %s has register copies before an exec restore:\n%s"
+    raise RuntimeError("isa gate: every variant of %s has code-generation findings:\n%s"
                        % (src, "\n".join(log)))
 
 

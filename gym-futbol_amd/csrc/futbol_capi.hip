@@ -596,3 +596,13 @@ extern "C" int futbol_stream_copy(const void* src, void* dst, uint64_t bytes, vo
     if (!src || !dst || (bytes & 15u)) return fail(nullptr, FUTBOL_EINVAL, "stream_copy: null buffer or bytes % 16");
     return launch_stream_copy(src, dst, (size_t)bytes, (hipStream_t)stream) == 0 ? FUTBOL_OK : FUTBOL_EHIP;
 }
+
+extern "C" int futbol_solver_layout(int32_t number_of_player, int32_t* out, int32_t n)
+{
+    if (!out || n < 1) return fail(nullptr, FUTBOL_EINVAL, "solver_layout: null out or n < 1");
+    if (!v1_supported(number_of_player)) return fail(nullptr, FUTBOL_EINVAL, "solver_layout: number_of_player");
+    int32_t o[8];
+    layout_v1(number_of_player, o);
+    for (int i = 0; i < n; ++i) out[i] = i < 8 ? o[i] : 0;
+    return FUTBOL_OK;
+}

@@ -82,6 +82,7 @@ int launch_v1(int N, int epw, int def, const V1Params* P, int B, const V1Ptrs& s
 int v1_supported(int N);
 int v1_supported_epw(int epw);
 size_t v1_spill_slots(int N);
+int layout_v1(int N, int32_t* o);  // 8 values, futbol_solver_layout
 bool v1_is_default_geometry(int N, const V1Params& p);
 
 int launch_v0(const V0Params* P, int B, const V0Ptrs& st, int out64, int what, const uint8_t* actions,

@@ -8,7 +8,8 @@ namespace futbol {
 #define FUTBOL_DECL(n)                                                                                    \
     int launch_v1_n##n##_e64(const V1Params* P, int B, const V1Ptrs& st, int out64, int what, int def,     \
                              const uint8_t* a, const uint8_t* mask, void* obs, void* reward, uint8_t* done, \
-                             void* term, int init, int nsteps, hipStream_t stream);
+                             void* term, int init, int nsteps, hipStream_t stream);                   \
+    void layout_v1_n##n##_e64(int32_t* o);
 FUTBOL_DECL(1)
 FUTBOL_DECL(2)
 FUTBOL_DECL(3)
@@ -35,6 +36,18 @@ int launch_v1(int N, int epw, int def, const V1Params* P, int B, const V1Ptrs& s
     FUTBOL_CASE(6) FUTBOL_CASE(7) FUTBOL_CASE(8) FUTBOL_CASE(9) FUTBOL_CASE(10)
 #undef FUTBOL_CASE
     default: return -2;
+    }
+}
+
+// futbol_solver_layout: the constants of the team size's own translation unit
+int layout_v1(int N, int32_t* o)
+{
+    switch (N) {
+#define FUTBOL_CASE(n) case n: layout_v1_n##n##_e64(o); return 0;
+    FUTBOL_CASE(1) FUTBOL_CASE(2) FUTBOL_CASE(3) FUTBOL_CASE(4) FUTBOL_CASE(5)
+    FUTBOL_CASE(6) FUTBOL_CASE(7) FUTBOL_CASE(8) FUTBOL_CASE(9) FUTBOL_CASE(10)
+#undef FUTBOL_CASE
+    default: return -1;
     }
 }
 

@@ -1497,6 +1497,13 @@ __device__ __forceinline__ void write_obs(const Env<N>& e, OT* o)
 #endif
 template <int N>
 constexpr bool kLateBias = N >= FUTBOL_LATE_BIAS_MIN;
+// diagnostic only (the round-4 "latec" build): the preloaded arbiter-cache
+// entries loaded after the action phase too
+#ifndef FUTBOL_LATE_CACHE_MIN
+#define FUTBOL_LATE_CACHE_MIN 99
+#endif
+template <int N>
+constexpr bool kLateCache = N >= FUTBOL_LATE_CACHE_MIN;
 
 template <int N, bool BIAS = true>
 __device__ __forceinline__ void load_bodies(const V1Ptrs& st, int env, int B, Env<N>& e)
@@ -1762,7 +1769,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
     load_bodies<N, !kLateBias<N>>(st, env, B, e);
     uint32_t ck[CKN<N>];
     double cj[CKN<N>];
-    load_cache_pre<N, EPW>(L, e.meta.ncache(), ck, cj);
+    if constexpr (!kLateCache<N>) load_cache_pre<N, EPW>(L, e.meta.ncache(), ck, cj);
     const double ep_ret0 = st.ep_ret[env];
     // lanes past B (last block) run the action phase on their shadow copy of env B-1 in
     // registers only (no store, no counter) and leave after the segment table is in LDS
@@ -1865,6 +1872,9 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
         sqneed |= ((uint64_t)(shoot_side & 1u) << (4 * N)) | ((uint64_t)(shoot_side >> 1) << (4 * N + 1)) |
                   ((uint64_t)(shoot_side != 0) << (4 * N + 2));
     }
+    // (the solver rows are free from the step's start until space_step's narrowphase stages the
+    // bodies in them: nothing is kept in them across steps or ROLL iterations)
+    static_assert(!kSqBatch<N> || sizeof(sh.rows) >= (size_t)kPowTabBytes, "pow tables fit the solver rows");
     if constexpr (kSqBatch<N>)
         glibc_pow2_need_lds<NSQ>(sqin, sq, sqneed, &sh.rows[0][0]);  // (rows: unused until space_step)
     sfor<2 * N>([&](auto K) {
@@ -1972,6 +1982,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
     store_seg<N, EPW>(seg_g, sh);
     if (!live) return;
     if constexpr (kLateBias<N>) load_bias<N>(st, env, B, e);
+    if constexpr (kLateCache<N>) load_cache_pre<N, EPW>(L, e.meta.ncache(), ck, cj);
     FUTBOL_CRUMB(L, 3);
     FUTBOL_STAMP(2);
 

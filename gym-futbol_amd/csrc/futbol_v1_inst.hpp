@@ -48,4 +48,17 @@ inline void launch_v1_step(const V1Params* P, int B, const V1Ptrs& st, int def, 
         }                                                                                                        \
         return hipGetLastError() == hipSuccess ? 0 : -1;                                                         \
     }                                                                                                            \
+    /* the solver layout THIS translation unit was compiled with (futbol_solver_layout) */                      \
+    void layout_v1_n##NP##_e64(int32_t* o)                                                                       \
+    {                                                                                                            \
+        constexpr int N = NP;                                                                                    \
+        o[0] = V1Shape<N>::K;                                                                                    \
+        o[1] = KXN<N>;                                                                                           \
+        o[2] = CKN<N>;                                                                                           \
+        o[3] = CBN<N>;                                                                                           \
+        o[4] = V1Shape<N>::P;                                                                                    \
+        o[5] = V1Shape<N>::ONE_ROWS ? 1 : 0;                                                                     \
+        o[6] = kSolveComponents<N> ? 1 : 0;                                                                      \
+        o[7] = kSqBatch<N> ? 1 : 0;                                                                              \
+    }                                                                                                            \
     }

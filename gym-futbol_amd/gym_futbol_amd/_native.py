@@ -60,6 +60,7 @@ SIGNATURES = [
     ("futbol_debug_stamps", C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32]),
     ("futbol_kernel_timing", C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     ("futbol_stream_copy", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
+    ("futbol_solver_layout", C.c_int, [C.c_int32, C.POINTER(C.c_int32), C.c_int32]),
 ]
 
 _lib = None
@@ -93,6 +94,18 @@ def default_config(env_kind, number_of_player=2):
     cfg = FutbolConfig()
     check(load().futbol_config_default(env_kind, number_of_player, C.byref(cfg)))
     return cfg
+
+
+SOLVER_LAYOUT_KEYS = ("lds_slots", "reg_spill", "cache_preload", "cache_batch", "arbiters", "one_rows",
+                      "components", "sq_batch")
+
+
+def solver_layout(number_of_player):
+    """The envs_v1 step kernel's solver layout for a team size, as compiled into the loaded library
+    (futbol_solver_layout; host-only, no GPU needed)."""
+    out = (C.c_int32 * len(SOLVER_LAYOUT_KEYS))()
+    check(load().futbol_solver_layout(number_of_player, out, len(SOLVER_LAYOUT_KEYS)))
+    return dict(zip(SOLVER_LAYOUT_KEYS, (int(v) for v in out)))
 
 
 class Context:

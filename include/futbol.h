@@ -165,6 +165,14 @@ int futbol_kernel_timing(FutbolCtx* ctx, int32_t mode, double* total_ms, int64_t
  * the 8 TB/s spec (Roofline). */
 int futbol_stream_copy(const void* src, void* dst, uint64_t bytes, void* stream);
 
+/* envs_v1 solver layout of the team size's compiled step kernel (host-only query, no GPU; for
+ * the parity tests, which must exercise every record path the build ships, and for diagnostics):
+ * out[0] LDS contact-record slots per env, [1] spill records held in registers through the solve,
+ * [2] arbiter-cache entries preloaded with the state, [3] cache entries per batched read past
+ * those, [4] arbiters per env (segment + pair), [5] one set of solver rows, [6] per-component
+ * split solve, [7] batched exact squares.  Writes min(n, 8) values (zeros past 8). */
+int futbol_solver_layout(int32_t number_of_player, int32_t* out, int32_t n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -27,24 +27,30 @@ LINE = re.compile(r"^\s+(\S.*?)\s*//\s*([0-9A-F]+):")
 FUNC = re.compile(r"^([0-9a-f]+) <(\S+)>:")
 
 
-def code_objects(path):
-    """gfx950 code object(s) of a HIP object file (its .hip_fatbin bundle), or the path itself if it is
-    already an AMDGPU ELF."""
+def code_objects(path, tmp, arch="gfx950"):
+    """the `arch` code object(s) of a HIP object file (its .hip_fatbin bundle, unbundled into the
+    directory tmp), or the path itself if it is already an AMDGPU ELF."""
     out = subprocess.run([LLVM + "/llvm-readelf", "-h", path], capture_output=True, text=True).stdout
     if "AMDGPU" in out:
         return [path]
     secs = subprocess.run([LLVM + "/llvm-readelf", "-S", path], capture_output=True, text=True).stdout
     if ".hip_fatbin" not in secs:
         return []  # host code only
-    tmp = tempfile.mkdtemp(prefix="isa_")
     fb = os.path.join(tmp, "fatbin")
     subprocess.run([LLVM + "/llvm-objcopy", "--dump-section=.hip_fatbin=" + fb, path, os.path.join(tmp, "x.o")],
                    check=True, capture_output=True)
-    co = os.path.join(tmp, "gfx950.elf")
+    co = os.path.join(tmp, arch + ".elf")
     subprocess.run([LLVM + "/clang-offload-bundler", "--type=o", "--input=" + fb,
-                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", "--output=" + co, "--unbundle"],
+                    "--targets=hipv4-amdgcn-amd-amdhsa--" + arch, "--output=" + co, "--unbundle"],
                    check=True, capture_output=True)
     return [co]
+
+
+def disassemble(path, arch="gfx950"):
+    """llvm-objdump -d listing(s) of the code object(s) of `path`"""
+    with tempfile.TemporaryDirectory(prefix="isa_") as tmp:
+        return [subprocess.run([LLVM + "/llvm-objdump", "-d", "--no-show-raw-insn", co], capture_output=True,
+                               text=True, check=True).stdout for co in code_objects(path, tmp, arch)]
 
 
 def scan(disasm):
@@ -99,11 +105,9 @@ def scan(disasm):
     return found
 
 
-def check_object(path):
+def check_object(path, arch="gfx950"):
     found = []
-    for co in code_objects(path):
-        dis = subprocess.run([LLVM + "/llvm-objdump", "-d", "--no-show-raw-insn", co], capture_output=True,
-                             text=True, check=True).stdout
+    for dis in disassemble(path, arch):
         found += scan(dis)
     return found
 

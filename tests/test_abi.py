@@ -74,3 +74,19 @@ def test_create_rejects_bad_arguments_without_touching_a_device(nat):
     cfg = nat.default_config(nat.ENV_V1, 2)
     assert lib.futbol_create(C.byref(cfg), 0, 0, 2**32 - 4, 8, C.byref(h)) == -1  # env ids > 32 bits
     assert lib.futbol_step(None, None, None, None, None, None, None) == -1
+
+
+def test_solver_layout_query(nat):
+    """futbol_solver_layout reports each team size's compiled record / cache layout (host-only): the
+    crowded-state parity test reads its slot counts from here, so they cannot drift from the build."""
+    lib = nat.load()
+    for n in range(1, 11):
+        lay = nat.solver_layout(n)
+        nb = 2 * n + 1
+        assert lay["arbiters"] == nb * 12 + nb * (nb - 1) // 2
+        assert 2 <= lay["lds_slots"] <= 8 and 0 <= lay["reg_spill"] <= 8
+        assert 1 <= lay["cache_preload"] <= lay["arbiters"] and lay["cache_batch"] >= 1
+        assert lay["one_rows"] in (0, 1) and lay["components"] == (1 if nb <= 8 else 0)
+    out = (C.c_int32 * 8)()
+    assert lib.futbol_solver_layout(0, out, 8) == -1 and lib.futbol_solver_layout(11, out, 8) == -1
+    assert lib.futbol_solver_layout(2, None, 8) == -1 and lib.futbol_solver_layout(2, out, 0) == -1

@@ -42,9 +42,12 @@ def _compare_state(venv, ora, n, B, tag):
     assert np.array_equal(ev, np.array([ora.envs[i].event for i in range(B)])), tag + ": rng event"
 
 
-# LDS record slots and register-held spill slots per team size (futbol_v1_impl.hpp V1Shape / KXN)
-LDS_SLOTS = {1: 8, 2: 7, 3: 6, 4: 5, 5: 4, 6: 3, 7: 2, 8: 4, 9: 3, 10: 2}
-REG_SPILL = {1: 0, 2: 0, 3: 0, 4: 0, 5: 4, 6: 0, 7: 0, 8: 0, 9: 0, 10: 0}
+def _layout(n):
+    """LDS record slots, register-held spill records and preloaded cache entries of the team size's
+    step kernel, read from the loaded library itself (futbol_solver_layout) -- hand-copied tables here
+    drifted from the shipped values once (round 4)"""
+    from gym_futbol_amd._native import solver_layout
+    return solver_layout(n)
 
 
 @pytest.mark.parametrize("n,B,T", [(2, 1024, 620), (5, 256, 320), (10, 64, 320), (1, 128, 310), (3, 128, 310),
@@ -108,8 +111,9 @@ def _crowded_states(n, B, seed):
         e.stamp = 50
         e.curr_dt = [0.1, 0.0001][int(rng.random() < 0.2)]
         e.current_time = 0.0
-        # up to 3x the kernel's register-preloaded cache entries (6 for N < 5, 8 for N >= 5), so that
-        # the lookups and the in-place compaction past the preloaded entries run on the first step
+        # up to 18 / 24 cached arbiters (N < 5 / N >= 5): more than the kernel's register-preloaded
+        # entries plus one batched read (futbol_solver_layout), so that the lookups and the in-place
+        # compaction past the preloaded entries run on the first step
         ckn = 8 if n >= 5 else 6
         for p in rng.choice(P, size=int(rng.integers(0, 3 * ckn + 1)), replace=False):
             p = int(p)
@@ -148,9 +152,11 @@ def _components(e, n):
     return len({find(b) for b in bodies})
 
 
-@pytest.mark.parametrize("n,B", [(2, 2048), (5, 512), (10, 128), (3, 512), (1, 256), (4, 256), (8, 128)])
+@pytest.mark.parametrize("n,B", [(2, 2048), (5, 512), (10, 128), (3, 512), (1, 256), (4, 256), (8, 128),
+                                 (6, 128), (7, 128), (9, 128)])
 def test_teacher_forced_crowded_states(n, B):
     seed = 100 + n
+    lay = _layout(n)
     ora = _crowded_states(n, B, seed)
     venv = _venv(n, B, seed)
     st = v1_oracle_to_state(ora.envs, n, B)
@@ -158,17 +164,21 @@ def test_teacher_forced_crowded_states(n, B):
     # the oracle must see exactly the state the kernel got (stamps are relative)
     v1_state_to_oracle(venv.get_state(), ora.envs, n, B)
     ex0, _, _ = v1_dense_cache(venv.get_state(), n, B)
-    assert ex0.sum(1).max() > (8 if n >= 5 else 6), "some env must hold more cache entries than are preloaded"
-    # contact records per env: past the LDS slots (K = 7 / 4 / 2 for N = 2 / 5 / 10) the solve holds
-    # the first spill records in registers (0 / 4 / 0 of them) and re-reads the rest from the global
-    # spill area in every sweep -- every one of these paths must run
-    lds_slots, reg_spill = LDS_SLOTS[n], REG_SPILL[n]
+    assert ex0.sum(1).max() > lay["cache_preload"] + lay["cache_batch"], \
+        "some env must hold more cache entries than are preloaded, past one batched read"
+    # contact records per env: past the LDS slots the solve holds the first spill records in
+    # registers and re-reads the rest from the global spill area in every sweep -- every one of
+    # these paths must run (the counts are the library's own, futbol_solver_layout)
+    lds_slots, reg_spill = lay["lds_slots"], lay["reg_spill"]
     most = comps = 0
+    per_env = np.zeros(B, np.int64)
     for t in range(3):
         a = venv.random_actions(900 + t, seed=4321)
         obs, rew, done, _ = venv.step(a)
         o2, r2, d2, _ = ora.step(a.cpu().numpy().astype(np.int32))
-        most = max(most, max(int(np.sum(np.asarray(e.arb_inlist))) for e in ora.envs))
+        cnt = np.array([int(np.sum(np.asarray(e.arb_inlist))) for e in ora.envs])
+        per_env = np.maximum(per_env, cnt)
+        most = max(most, int(cnt.max()))
         if n <= 3:  # the per-component split solve (Nb <= 8) must see multi-component envs
             comps = max(comps, max(_components(e, n) for e in ora.envs))
         assert np.array_equal(done.cpu().numpy(), d2)
@@ -181,6 +191,9 @@ def test_teacher_forced_crowded_states(n, B):
     if n > 1:  # 1v1 (3 bodies) never holds more than its 8 LDS slots in practice
         assert ex.sum(1).max() > 8, "crowded states must overflow the LDS contact slots"
         assert most > lds_slots + reg_spill, "some env must have records past the register-held spill slots"
+        if reg_spill:  # an env whose spill records all fit the register-held ones, too
+            assert ((per_env > lds_slots) & (per_env <= lds_slots + reg_spill)).any(), \
+                "some env must spill into the register-held records only"
     else:
         assert most >= lds_slots - 2, "some 1v1 env must come close to filling its LDS slots"
     assert n > 3 or comps >= 2, "some env must have a contact graph of two or more components"
