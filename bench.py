@@ -265,7 +265,9 @@ STAMP_SLOTS = ["load state", "actions + opponent RNG", "process_action + out-of-
                "arbiter cache update", "reward / goal / time", "goal reset + auto-reset phases", "obs + store"]
 STAMP_STRIDE = 32  # u64 slots per wave (futbol_kernels.hpp kStampStride)
 SUB_SLOTS = {16: "integrate p", 17: "collide: stage rows", 18: "collide: hit tests (segments, pairs)",
-             19: "solve: publish rows / records / work list"}
+             19: "solve: publish rows / records / work list", 20: "process_action: exact squares (batch)",
+             21: "process_action: player loop", 22: "cache lookups past the preloaded entries"}
+# (slot 2 is then the out-of-bounds test + segment-table store, slot 5 integrate v + clamp)
 
 
 def stamps_report(venv, one_step, args):

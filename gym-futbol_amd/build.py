@@ -186,12 +186,26 @@ def _compile(src, force):
                        % (src, "\n".join(log)))
 
 
+# A/B variants of a few TUs: FUTBOL_VARIANT_TUS="futbol_v1_n2_e64.hip futbol_v1_n5_e64.hip" compiles only
+# those with the variant's flags and links the product's objects (build/obj) for the others
+VARIANT_TUS = set(os.environ.get("FUTBOL_VARIANT_TUS", "").split())
+PRODUCT_OBJ = os.path.join(HERE, "build", "obj")
+
+
 def build(force=False, jobs=None, verbose=True):
     os.makedirs(OBJ, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     jobs = jobs or min(8, os.cpu_count() or 4)
+
+    def one(src):
+        if VARIANT and VARIANT_TUS and os.path.basename(src) not in VARIANT_TUS:
+            obj = os.path.join(PRODUCT_OBJ, os.path.basename(src) + ".o")
+            if not os.path.exists(obj):
+                raise RuntimeError("FUTBOL_VARIANT_TUS: build the product first (%s missing)" % obj)
+            return obj
+        return _compile(src, force)
     with ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, force), srcs))
+        objs = list(ex.map(one, srcs))
     if force or _stale(LIB, objs):
         cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)

@@ -363,11 +363,15 @@ __host__ __device__ __forceinline__ double glibc_pow2_full(double x, const doubl
 // bound); h = x*x, l = fma(x, x, -h) its exact rounding error
 __host__ __device__ __forceinline__ bool pow2_near_midpoint(double h, double l)
 {
-    // ulp(h) / 2 * (1 - 2^-5) = 2^(e - 53) * (1 - 2^-5), e the exponent of h (h normal, e >= -969:
-    // smaller squares go to the full path, which returns x*x for them)
-    const uint64_t eb = f64_to_bits(h) & 0x7ff0000000000000ull;
-    const double near = bits_to_f64(eb > (54ull << 52) ? eb - (53ull << 52) : 0ull) * (1.0 - 0x1.0p-5);
-    return !(__builtin_fabs(l) < near) && h != 0.0;
+    // ulp(h) / 2 * (1 - 2^-5) = 2^(E - 53) * (1 - 2^-5) for h = m 2^E, m in [1, 2): frexp's exponent is
+    // E + 1 (v_frexp_exp_i32_f64 + v_ldexp_f64 on the GPU: 2 instructions instead of the exponent-field
+    // arithmetic, compare and select).  h = 0 (x = 0, common: aligned bodies): e = 0, near > 0 = |l|, not
+    // near.  Tiny, infinite or NaN h may be reported near or not -- glibc's full path returns x*x for
+    // them (glibc_pow2_full's topx test), so the square is x*x either way
+    int e;
+    (void)__builtin_frexp(h, &e);
+    const double near = __builtin_ldexp(1.0 - 0x1.0p-5, e - 54);
+    return !(__builtin_fabs(l) < near);
 }
 
 // glibc pow(x, 2.0)
@@ -460,7 +464,9 @@ __device__ __forceinline__ void stage_pow_tables(void* lds, const double*& logt,
 }
 
 // glibc_pow2_need (below) with the tables staged in LDS (stage_pow_tables into `lds`) when some lane
-// of the wave needs glibc's path: two LDS lookups per slow round instead of two global ones
+// of the wave needs glibc's path: two LDS lookups per slow round instead of two global ones.  (Loading
+// the tables' chunks with the step's state instead, so that staging waits for no memory at the use,
+// measured 2v2 +2.8% (22.51 -> 23.15 us, 20 more live VGPRs), 5v5 neutral: not adopted, round 5.)
 template <int M>
 __device__ __forceinline__ void glibc_pow2_need_lds(const double (&x)[M], double (&h)[M], uint64_t need, void* lds);
 

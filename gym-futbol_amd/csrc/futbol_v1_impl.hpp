@@ -88,12 +88,16 @@ constexpr int KXN = N == 5 ? FUTBOL_SPILL_REGS : (N >= 6 ? FUTBOL_SPILL_REGS_BIG
 // envs_v1's exact squares (glibc pow) as one batch per site with LDS-staged tables (N <= 5), or one
 // body / player at a time with the tables read from global memory (N >= 6: the large instances run at
 // the register limit, where the batches' arrays added spills and the code-generation faults moved in)
+#ifndef FUTBOL_SQ_BATCH_MAX  // diagnostic knob (the round-4 N = 6 build batched every N's squares)
+#define FUTBOL_SQ_BATCH_MAX 5
+#endif
 template <int N>
-constexpr bool kSqBatch = N <= 5;
+constexpr bool kSqBatch = N <= FUTBOL_SQ_BATCH_MAX;
 
 // Diagnostic build only (-DFUTBOL_STAMPS, bench.py --stamps): per-wave s_memtime at phase
 // boundaries, accumulated into st.stamps[wave][slot] (kStampStride slots per wave: 0-10 phases,
-// 11-14 the launch snapshot, 15 solver records, 16-23 sub-phases).  Never compiled into the product.
+// 11-14 the launch snapshot, 15 solver records, 16-23 sub-phases: 16-19 space_step, 20-21 the action
+// phase's squares and player loop, 22 the cache lookups).  Never compiled into the product.
 #ifdef FUTBOL_STAMPS
 #define FUTBOL_STAMP(slot)                                                                                \
     do {                                                                                                  \
@@ -976,6 +980,7 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
         }
     }
 
+    FUTBOL_STAMP(dtc == 2 ? 22 : 9);
     // cpBodyUpdateVelocity + the reference's limit_velocity callback (ball.py:49-56, player.py:45-52):
     // l = Vec2d.length = sqrt(vx**2 + vy**2) with Python's `**2` = glibc pow(x, 2), and
     // l > vmax  <=>  s2 > T (T = largest double whose rounded sqrt is <= vmax).  x*x decides every
@@ -1877,6 +1882,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
     static_assert(!kSqBatch<N> || sizeof(sh.rows) >= (size_t)kPowTabBytes, "pow tables fit the solver rows");
     if constexpr (kSqBatch<N>)
         glibc_pow2_need_lds<NSQ>(sqin, sq, sqneed, &sh.rows[0][0]);  // (rows: unused until space_step)
+    FUTBOL_STAMP(20);
     sfor<2 * N>([&](auto K) {
         constexpr int k = K;
         constexpr int side = k < N ? 0 : 1;
@@ -1943,6 +1949,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
         e.vy[BL] = dribble ? e.vy[k] : (kick ? kvy : e.vy[BL]);
         owner = tk ? (uint32_t)side : owner;
     });
+    FUTBOL_STAMP(21);
 
     // check_and_fix_out_bounds (:247-287), before physics
     bool out = false;
