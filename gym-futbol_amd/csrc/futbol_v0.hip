@@ -42,17 +42,51 @@ struct Env {
 // glibc pow(x, 2.0)'s tables (futbol_powtab.h), staged in LDS by every step launch: the near-midpoint
 // squares (glibc_sq2) look them up twice in dependent succession, and some lane of a wave needs that
 // at nearly every get_vec
-__shared__ double s_pow_log[128 * 3];
-__shared__ uint64_t s_pow_exp[256];
+alignas(16) __shared__ double s_pow_log[128 * 3];
+alignas(16) __shared__ uint64_t s_pow_exp[256];
 // and glibc's sin / cos table (resolve_shot: some lane of nearly every wave shoots)
-__shared__ double s_sincos[440];
+alignas(16) __shared__ double s_sincos[440];
 
+// A/B option (round 5): the tables copied by LDS-DMA (global_load_lds_dwordx4, no registers), issued
+// before the step's state loads and waited for with them -- one memory round trip per step instead of
+// the copy's own round trip ahead of the state's
+#ifndef FUTBOL_V0_GLDS
+#define FUTBOL_V0_GLDS 0
+#endif
 __device__ __forceinline__ void stage_pow_tables()
 {
+#if FUTBOL_V0_GLDS
+    typedef __attribute__((address_space(3))) void lds_void;
+    const int lane = (int)threadIdx.x;  // (a one-wave block, every lane active)
+    const uint4* pl = reinterpret_cast<const uint4*>(kPowLog);
+    const uint4* pe = reinterpret_cast<const uint4*>(kPowExp);
+    const uint4* ps = reinterpret_cast<const uint4*>(kSinCosTab);
+    char* dl = reinterpret_cast<char*>(s_pow_log);
+    char* de = reinterpret_cast<char*>(s_pow_exp);
+    char* ds = reinterpret_cast<char*>(s_sincos);
+    static_assert(sizeof(s_pow_log) == 3 * 1024 && sizeof(s_pow_exp) == 2 * 1024 && sizeof(s_sincos) == 3 * 1024 + 448,
+                  "DMA pieces");
+#pragma unroll
+    for (int j = 0; j < 3; ++j) __builtin_amdgcn_global_load_lds(pl + 64 * j + lane, (lds_void*)(dl + 1024 * j), 16, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) __builtin_amdgcn_global_load_lds(pe + 64 * j + lane, (lds_void*)(de + 1024 * j), 16, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) __builtin_amdgcn_global_load_lds(ps + 64 * j + lane, (lds_void*)(ds + 1024 * j), 16, 0, 0);
+    if (lane < 28) __builtin_amdgcn_global_load_lds(ps + 192 + lane, (lds_void*)(ds + 3072), 16, 0, 0);
+#else
     for (int k = threadIdx.x; k < 128 * 3; k += 64) s_pow_log[k] = kPowLog[k];
     for (int k = threadIdx.x; k < 256; k += 64) s_pow_exp[k] = kPowExp[k];
     for (int k = threadIdx.x; k < 440; k += 64) s_sincos[k] = kSinCosTab[k];
     __syncthreads();
+#endif
+}
+// (FUTBOL_V0_GLDS) before the first table read: the DMA has landed
+__device__ __forceinline__ void pow_tables_ready()
+{
+#if FUTBOL_V0_GLDS
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#endif
 }
 
 // get_vec (:62-65): vector from o to t and its magnitude; `vec[0]**2` is numpy's float64 power,
@@ -499,6 +533,7 @@ __device__ __forceinline__ void v0_step_body(const V0Params* __restrict__ P, con
         a0 = a0 > 3 ? 3 : a0;
         a1 = a1 > 3 ? 3 : a1;
     }
+    pow_tables_ready();  // (the tables' DMA was issued before the state loads; every later read is after here)
 
     double ob[5], oa1[5], oa2[5], oown[5];
     const int oidx = e.owner <= 3 ? (int)e.owner : 4;

@@ -75,6 +75,8 @@ def defs_uses(text):
     mn = text.split()[0]
     rest = text[len(mn):].strip()
     ops = [o.strip() for o in rest.split(",")] if rest else []
+    if mn.startswith("global_load_lds") or (mn.startswith("buffer_load") and re.search(r"\blds\b", rest)):
+        return [], [r for o in ops for r in regs(o)]  # LDS-DMA: the data goes to LDS, no register written
     if NO_DEF.match(mn + " "):
         d = []
         u = [r for o in ops for r in regs(o)]
