@@ -463,36 +463,13 @@ __device__ __forceinline__ void stage_pow_tables(void* lds, const double*& logt,
     expt = reinterpret_cast<const uint64_t*>(d + NL);
 }
 
-// The pow tables copied into `lds` by LDS-DMA (global_load_lds_dwordx4: 5 x 16 bytes per lane, no
-// registers), issued at the top of a step with the state's loads so that they land during its memory
-// round trip; every lane of the wave must be active (the DMA writes base + lane * 16).  A later reader
-// waits with pow_tables_glds_wait().
-__device__ __forceinline__ void pow_tables_glds(void* lds)
-{
-    typedef __attribute__((address_space(3))) void lds_void;
-    const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-    const uint4* sl = reinterpret_cast<const uint4*>(kPowLog);
-    const uint4* se = reinterpret_cast<const uint4*>(kPowExp);
-    char* d = static_cast<char*>(lds);
-    __builtin_amdgcn_global_load_lds(sl + lane, (lds_void*)(d), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds(sl + 64 + lane, (lds_void*)(d + 1024), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds(sl + 128 + lane, (lds_void*)(d + 2048), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds(se + lane, (lds_void*)(d + 3072), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds(se + 64 + lane, (lds_void*)(d + 4096), 16, 0, 0);
-}
-__device__ __forceinline__ void pow_tables_glds_wait()
-{
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the DMA has written LDS
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 // glibc_pow2_need (below) with the tables staged in LDS (stage_pow_tables into `lds`) when some lane
 // of the wave needs glibc's path: two LDS lookups per slow round instead of two global ones.  (Loading
 // the tables' chunks with the step's state instead, so that staging waits for no memory at the use,
-// measured 2v2 +2.8% (22.51 -> 23.15 us, 20 more live VGPRs), 5v5 neutral: not adopted, round 5.)
+// measured 2v2 +2.8% (22.51 -> 23.15 us, 20 more live VGPRs), 5v5 neutral; copied by LDS-DMA at the
+// step's start instead -- the v0 kernel's form: 2v2 -0.4%, 5v5 +0.4%; neither adopted, round 5.)
 template <int M>
-__device__ __forceinline__ void glibc_pow2_need_lds(const double (&x)[M], double (&h)[M], uint64_t need, void* lds,
-                                                    bool staged = false);
+__device__ __forceinline__ void glibc_pow2_need_lds(const double (&x)[M], double (&h)[M], uint64_t need, void* lds);
 
 // h[i] = glibc pow(x[i], 2.0) for the squares whose bit i of `need` is set, x*x for the others
 // (squares whose value cannot matter for this lane: the caller's superset of the used ones).  Like
@@ -526,8 +503,7 @@ __host__ __device__ __forceinline__ void glibc_pow2_need(const double (&x)[M], d
 }
 
 template <int M>
-__device__ __forceinline__ void glibc_pow2_need_lds(const double (&x)[M], double (&h)[M], uint64_t need, void* lds,
-                                                    bool staged)
+__device__ __forceinline__ void glibc_pow2_need_lds(const double (&x)[M], double (&h)[M], uint64_t need, void* lds)
 {
     static_assert(M <= 64, "pending mask");
     uint64_t pend = 0;
@@ -548,13 +524,7 @@ __device__ __forceinline__ void glibc_pow2_need_lds(const double (&x)[M], double
         logt = kPowLog;
         expt = kPowExp;
 #else
-        if (staged) {  // (pow_tables_glds at the step's start)
-            pow_tables_glds_wait();
-            logt = static_cast<const double*>(lds);
-            expt = reinterpret_cast<const uint64_t*>(static_cast<char*>(lds) + sizeof(kPowLog));
-        } else {
-            stage_pow_tables(lds, logt, expt);
-        }
+        stage_pow_tables(lds, logt, expt);
 #endif
         while (pend != 0u) {
             const uint64_t bit = pend & (0ull - pend);

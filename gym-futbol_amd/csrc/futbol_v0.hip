@@ -47,17 +47,14 @@ alignas(16) __shared__ uint64_t s_pow_exp[256];
 // and glibc's sin / cos table (resolve_shot: some lane of nearly every wave shoots)
 alignas(16) __shared__ double s_sincos[440];
 
-// A/B option (round 5): the tables copied by LDS-DMA (global_load_lds_dwordx4, no registers), issued
-// before the step's state loads and waited for with them -- one memory round trip per step instead of
-// the copy's own round trip ahead of the state's
-#ifndef FUTBOL_V0_GLDS
-#define FUTBOL_V0_GLDS 0
-#endif
+// The tables are copied by LDS-DMA (global_load_lds_dwordx4: 16 bytes per lane and instruction, no
+// registers), issued before the step's state loads and waited for with them (pow_tables_ready): one
+// memory round trip per step.  Round 4 copied them with plain loads, ds_writes and a barrier first --
+// a round trip of its own ahead of the state's: C3 21.98 -> 20.01 us (round 5, profiles/r05/ab/).
 __device__ __forceinline__ void stage_pow_tables()
 {
-#if FUTBOL_V0_GLDS
     typedef __attribute__((address_space(3))) void lds_void;
-    const int lane = (int)threadIdx.x;  // (a one-wave block, every lane active)
+    const int lane = (int)threadIdx.x;  // (a one-wave block: every lane is active here)
     const uint4* pl = reinterpret_cast<const uint4*>(kPowLog);
     const uint4* pe = reinterpret_cast<const uint4*>(kPowExp);
     const uint4* ps = reinterpret_cast<const uint4*>(kSinCosTab);
@@ -73,20 +70,13 @@ __device__ __forceinline__ void stage_pow_tables()
 #pragma unroll
     for (int j = 0; j < 3; ++j) __builtin_amdgcn_global_load_lds(ps + 64 * j + lane, (lds_void*)(ds + 1024 * j), 16, 0, 0);
     if (lane < 28) __builtin_amdgcn_global_load_lds(ps + 192 + lane, (lds_void*)(ds + 3072), 16, 0, 0);
-#else
-    for (int k = threadIdx.x; k < 128 * 3; k += 64) s_pow_log[k] = kPowLog[k];
-    for (int k = threadIdx.x; k < 256; k += 64) s_pow_exp[k] = kPowExp[k];
-    for (int k = threadIdx.x; k < 440; k += 64) s_sincos[k] = kSinCosTab[k];
-    __syncthreads();
-#endif
 }
-// (FUTBOL_V0_GLDS) before the first table read: the DMA has landed
+// before the first table read: the DMA has landed (vmcnt(0): the state's loads, issued after it, are
+// waited for at this point anyway)
 __device__ __forceinline__ void pow_tables_ready()
 {
-#if FUTBOL_V0_GLDS
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#endif
 }
 
 // get_vec (:62-65): vector from o to t and its magnitude; `vec[0]**2` is numpy's float64 power,

@@ -88,10 +88,6 @@ constexpr int KXN = N == 5 ? FUTBOL_SPILL_REGS : (N >= 6 ? FUTBOL_SPILL_REGS_BIG
 // envs_v1's exact squares (glibc pow) as one batch per site with LDS-staged tables (N <= 5), or one
 // body / player at a time with the tables read from global memory (N >= 6: the large instances run at
 // the register limit, where the batches' arrays added spills and the code-generation faults moved in)
-// A/B option (round 5): the action phase's pow tables by LDS-DMA at the step's start
-#ifndef FUTBOL_POW_GLDS
-#define FUTBOL_POW_GLDS 0
-#endif
 #ifndef FUTBOL_SQ_BATCH_MAX  // diagnostic knob (the round-4 N = 6 build batched every N's squares)
 #define FUTBOL_SQ_BATCH_MAX 5
 #endif
@@ -1756,11 +1752,6 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
     // actions and the meta word (the opponent's draws need only these), then the body state,
     // the first CK arbiter-cache entries and the running return
     const SegLds seg_g = fetch_seg(P);
-#if FUTBOL_POW_GLDS
-    // the action phase's exact squares: glibc's pow tables into the (still free) solver rows by LDS-DMA,
-    // landing during the state's memory round trip instead of a round trip of their own at the use
-    if constexpr (kSqBatch<N>) pow_tables_glds(&sh.rows[0][0]);
-#endif
     uint32_t araw[2 * N];
     if constexpr ((2 * N) % 4 == 0) {
         const uint32_t* a32 = (const uint32_t*)(actions + (size_t)env * (2 * N));
@@ -1890,7 +1881,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
     // bodies in them: nothing is kept in them across steps or ROLL iterations)
     static_assert(!kSqBatch<N> || sizeof(sh.rows) >= (size_t)kPowTabBytes, "pow tables fit the solver rows");
     if constexpr (kSqBatch<N>)
-        glibc_pow2_need_lds<NSQ>(sqin, sq, sqneed, &sh.rows[0][0], FUTBOL_POW_GLDS != 0);  // (rows: unused until space_step)
+        glibc_pow2_need_lds<NSQ>(sqin, sq, sqneed, &sh.rows[0][0]);  // (rows: unused until space_step)
     FUTBOL_STAMP(20);
     sfor<2 * N>([&](auto K) {
         constexpr int k = K;

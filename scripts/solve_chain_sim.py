@@ -107,8 +107,9 @@ def strategies(comps_per_env, A=64):
     def bucket(x):  # long items first by 4 length classes (stable within a class)
         return 0 if x >= 5 else (1 if x >= 3 else (2 if x == 2 else 3))
     items_b = sorted(items_comp, key=bucket)
+    rounds_global = (-(-len(items_whole) // A)) * (max(items_whole) if items_whole else 0)  # today's code
     return (_rounds(items_whole, A), _rounds(items_comp, A), _rounds(sorted(items_comp, reverse=True), A), best,
-            _rounds(items_b, A))
+            _rounds(items_b, A), rounds_global, _rounds(sorted(items_whole, reverse=True), A))
 
 
 def main():
@@ -128,7 +129,8 @@ def main():
     rng = np.random.default_rng(1234)
     W = B // 64
     whole_w, comp_w, items_w, spill_w = [], [], [], []
-    strat = {"whole": [], "comp": [], "comp_sort": [], "split": [], "comp_bucket4": []}
+    strat = {"whole": [], "comp": [], "comp_sort": [], "split": [], "comp_bucket4": [], "whole_globalm": [],
+             "whole_sorted": []}
     K = a.lds_slots if a.lds_slots is not None else 4
     for t in range(a.steps):
         ora.step(rng.integers(0, 5, (B, 2 * n), dtype=np.int32), nthreads=a.threads)
@@ -142,7 +144,8 @@ def main():
             for w in range(W):
                 pc_ = percomp[64 * w:64 * w + 64]
                 rows.append(strategies([list(x[x > 0]) for x in pc_]))
-            for k_, v_ in zip(("whole", "comp", "comp_sort", "split", "comp_bucket4"), np.array(rows).T):
+            for k_, v_ in zip(("whole", "comp", "comp_sort", "split", "comp_bucket4", "whole_globalm", "whole_sorted"),
+                              np.array(rows).T):
                 strat[k_].append(v_)
         if a.lds_slots is not None:
             spill_w.append((rec > a.lds_slots).reshape(W, 64).any(1))
