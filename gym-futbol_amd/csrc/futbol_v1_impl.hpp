@@ -1087,6 +1087,24 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
                 total = (int)ct;
             }
         }
+        // two halves per env (N = 4..7): when more than A / 2 envs have contacts the items take two
+        // rounds of the lanes, each as long as its longest item -- so the items are published longest
+        // first (envs with spill records, then K, K - 1, ... LDS records), and each round runs for its
+        // own longest item (mr below): round 2 holds the short ones.  Item order does not change any
+        // result (an item is one lane's serial chain over its own env's rows)
+        constexpr bool kSortItems = !kSolveComponents<N> && !S::ONE_ROWS;
+        if constexpr (kSortItems) {
+            const int cls = n > KL ? 0 : KL + 1 - n;
+            uint32_t before = 0, pos = 0;
+#pragma unroll
+            for (int v = 0; v <= KL; ++v) {
+                const uint64_t mb = __ballot(n > 0 && cls == v);
+                const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, 0u));
+                pos = cls == v ? before + r : pos;
+                before += (uint32_t)__popcll(mb);
+            }
+            cbase = pos;
+        }
         // the wave's longest item (records): m
         int msz = 0;
 #pragma unroll
@@ -1155,7 +1173,19 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
             }
             for (int i0 = 0; i0 < items; i0 += A) {
                 const int it_ = i0 + w;
+                int mr = m;  // this round's longest item
+                if (kSortItems && items > A) {
+                    const uint32_t e0 = it_ < items ? sh->item[it_ >> 1] : 0u;
+                    const int sz = __popc((e0 >> 6) & 0xffu);
+                    mr = 0;
+#pragma unroll
+                    for (int b = 3; b >= 0; --b) {
+                        const int t = mr | (1 << b);
+                        if (t <= KL && __ballot(sz >= t)) mr = t;
+                    }
+                }
                 if (it_ < items) {
+                    const int m = mr;
                     const uint32_t ent = sh->item[S::ONE_ROWS ? it_ : it_ >> 1];
                     const int ie = (int)(ent & 63u);
                     const int h = S::ONE_ROWS ? 1 - pass : it_ & 1;

@@ -109,7 +109,9 @@ def strategies(comps_per_env, A=64):
     items_b = sorted(items_comp, key=bucket)
     rounds_global = (-(-len(items_whole) // A)) * (max(items_whole) if items_whole else 0)  # today's code
     return (_rounds(items_whole, A), _rounds(items_comp, A), _rounds(sorted(items_comp, reverse=True), A), best,
-            _rounds(items_b, A), rounds_global, _rounds(sorted(items_whole, reverse=True), A))
+            _rounds(items_b, A), rounds_global, _rounds(sorted(items_whole, reverse=True), A),
+            max(items_comp, default=0) if len(items_comp) <= A else rounds_global,  # today's N <= 3 rule
+            max(items_comp, default=0) if len(items_comp) <= A else _rounds(sorted(items_whole, reverse=True), A))
 
 
 def main():
@@ -130,7 +132,7 @@ def main():
     W = B // 64
     whole_w, comp_w, items_w, spill_w = [], [], [], []
     strat = {"whole": [], "comp": [], "comp_sort": [], "split": [], "comp_bucket4": [], "whole_globalm": [],
-             "whole_sorted": []}
+             "whole_sorted": [], "n23_today": [], "n23_fallback_sorted": []}
     K = a.lds_slots if a.lds_slots is not None else 4
     for t in range(a.steps):
         ora.step(rng.integers(0, 5, (B, 2 * n), dtype=np.int32), nthreads=a.threads)
@@ -144,7 +146,8 @@ def main():
             for w in range(W):
                 pc_ = percomp[64 * w:64 * w + 64]
                 rows.append(strategies([list(x[x > 0]) for x in pc_]))
-            for k_, v_ in zip(("whole", "comp", "comp_sort", "split", "comp_bucket4", "whole_globalm", "whole_sorted"),
+            for k_, v_ in zip(("whole", "comp", "comp_sort", "split", "comp_bucket4", "whole_globalm", "whole_sorted",
+                               "n23_today", "n23_fallback_sorted"),
                               np.array(rows).T):
                 strat[k_].append(v_)
         if a.lds_slots is not None:
