@@ -263,6 +263,40 @@ __device__ __forceinline__ void info_rows(unsigned long long info, uint32_t& ao,
     ao = a * ROW;
     bo = (bcode < 32u ? bcode : (uint32_t)V1Shape<N>::Nb) * ROW;
 }
+// the info word `contact` stores for arbiter id pid (its bodies follow from the id: segment arbiters
+// body * 12 + segment, circle pairs Nb * 12 + row-major pair index), so that a record's flag can be set
+// without reading the record back (a spill record is a global round trip)
+template <int N>
+__device__ __forceinline__ long long info_of_pid(int pid, bool normal)
+{
+    using S = V1Shape<N>;
+    const bool segc = pid < S::Nb * kNSeg;
+    const int q = pid - S::Nb * kNSeg;
+    int i = 0;
+    sfor<1, S::Nb - 1>([&](auto K) {
+        constexpr int k = K;
+        i += q >= k * S::Nb - k * (k + 1) / 2 ? 1 : 0;
+    });
+    const int as = pid / kNSeg;
+    const int a = segc ? as : i;
+    const int bcode = segc ? 32 + (pid - as * kNSeg) : q - (i * S::Nb - i * (i + 1) / 2) + i + 1;
+    return pack_info(a, bcode, pid, normal);
+}
+// Record lookups by arbiter id from the hit masks (slot_of, info_of_pid below) instead of scans that
+// read every record back -- the owner's cache attach, the lookups past the preloaded entries and the
+// cache filter -- and the cache update's spill reads in batches: the 5v5 instance (4 LDS record slots:
+// the crowded envs' records spill), 50.6 -> 50.1 us.  Measured slower where spill records are rare
+// (2v2 22.26 -> 22.66 us, 3v3 +1.4%: the hit masks are live through the solve), and every build
+// variant of the 10v10 kernel with it had lost-value findings (the liveness gate, section 6): the
+// other instances keep the scans
+#ifndef FUTBOL_HM_MIN
+#define FUTBOL_HM_MIN 5
+#endif
+#ifndef FUTBOL_HM_MAX
+#define FUTBOL_HM_MAX 5
+#endif
+template <int N>
+constexpr bool kHitMask = N >= FUTBOL_HM_MIN && N <= FUTBOL_HM_MAX;
 // null record (slots between a lane's contact count and the wave's): both bodies static (a = Z)
 template <int N>
 __device__ __forceinline__ long long null_info()
@@ -310,6 +344,12 @@ struct Lane {
         }
     }
     __device__ __forceinline__ int get_info(int s) const { return (int)__double_as_longlong(get(s, 1).y); }
+    // the info word of record s alone (no read of the record: see info_of_pid)
+    __device__ __forceinline__ void put_info(int s, long long info) const
+    {
+        if (s < KL) sh->rec[s][1][lane].y = __longlong_as_double(info);
+        else *sp(s, 3) = __longlong_as_double(info);
+    }
     __device__ __forceinline__ double get_jn(int s) const { return get(s, 3).y; }
     __device__ __forceinline__ void set_rec(int s, double nx, double ny, double nm, double bi, double bo, double j,
                                             long long info) const
@@ -709,6 +749,30 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
     auto pid_of = [&](int word, int bit, bool segw) {  // arbiter id of a hit bit
         return segw ? word * BPW * kNSeg + bit : S::Nb * kNSeg + word * 64 + bit;
     };
+    // the record slot of arbiter pid (its rank among this step's hits, which are the records in
+    // canonical order), or -1 when it is not a contact of this step: a test of the hit masks instead of
+    // a scan of the records (whose spill lines are a global round trip each)
+    auto slot_of = [&](int pid) -> int {
+        constexpr int SW = BPW * kNSeg;  // segment hit bits per word
+        const bool segc = pid < S::Nb * kNSeg;
+        const int q = pid - S::Nb * kNSeg;
+        const int w = segc ? pid / SW : NWS + (q >> 6);
+        const int bit = segc ? pid - (pid / SW) * SW : (q & 63);
+        uint64_t word = 0;
+        int pre = 0;
+        sfor<NWS>([&](auto WD) {
+            constexpr int x = WD;
+            word = w == x ? hsw[x] : word;
+            pre += x < w ? __popcll(hsw[x]) : 0;
+        });
+        sfor<NPW>([&](auto Q) {
+            constexpr int x = NWS + (int)Q;
+            word = w == x ? hpw[Q] : word;
+            pre += x < w ? __popcll(hpw[Q]) : 0;
+        });
+        const bool hit = (word >> bit) & 1ull;
+        return hit ? pre + __popcll(word & ((1ull << bit) - 1ull)) : -1;
+    };
     // the contact and record of hit `pid` of env column o (env id oenv), record slot r
     auto contact = [&](int o, int oenv, int pid, int r, bool attach) {
         // CircleToSegment (circle a, segment sg: the second body is the static one) and
@@ -884,7 +948,44 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // the owner attaches the cached jnAcc and the NORMAL (warm start) flag to its records
+        // the owner attaches the cached jnAcc and the NORMAL (warm start) flag to its records: the
+        // hits in canonical order are the records in slot order, so nothing is read back
+        if constexpr (kHitMask<N>) {
+        int s = 0;
+        auto attach_rec = [&](int pid) {
+            double jn = 0.0;
+            bool hit = false, normal = false;
+#pragma unroll
+            for (int c = 0; c < CKN<N>; ++c)
+                if ((int)(ck[c] & 0x3ffu) == pid) {
+                    jn = cj[c];
+                    hit = true;
+                    normal = (ck[c] >> 12) == 0;
+                    touched |= 1u << c;
+                }
+            if (hit) {
+                L.put(s, 3, make_double2(0.0, jn));
+                if (normal) L.put_info(s, info_of_pid<N>(pid, true));
+            }
+            ++s;
+        };
+        sfor<NWS>([&](auto WD) {
+            uint64_t h = hsw[WD];
+            while (h) {
+                const int bit = __builtin_ctzll(h);
+                h &= h - 1;
+                attach_rec(pid_of(WD, bit, true));
+            }
+        });
+        sfor<NPW>([&](auto Q) {
+            uint64_t h = hpw[Q];
+            while (h) {
+                const int bit = __builtin_ctzll(h);
+                h &= h - 1;
+                attach_rec(pid_of(Q, bit, false));
+            }
+        });
+        } else {
         for (int s = 0; s < n; ++s) {
             const double2 r1 = L.get(s, 1);
             const int pid = (int)((__double_as_longlong(r1.y) >> 11) & 511);
@@ -903,6 +1004,7 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
                 if (normal)
                     L.put(s, 1, make_double2(r1.x, __longlong_as_double(__double_as_longlong(r1.y) | (1ll << 20))));
             }
+        }
         }
     } else {  // more hits than table entries: every lane computes its own contacts
         int r = 0;
@@ -965,6 +1067,17 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
                 jn[i] = L.cjn[(size_t)c * B + env];
                 key[i] = c0 + i < ncache ? k : 0xffffu;
             }
+            if constexpr (kHitMask<N>) {
+#pragma unroll
+            for (int i = 0; i < CBN<N>; ++i) {
+                const int pid = (int)(key[i] & 0x3ffu);
+                const int s = key[i] != 0xffffu ? slot_of(pid) : -1;
+                if (s >= 0) {
+                    L.put(s, 3, make_double2(0.0, jn[i]));
+                    if ((key[i] >> 12) == 0) L.put_info(s, info_of_pid<N>(pid, true));
+                }
+            }
+            } else {
             for (int s = 0; s < n; ++s) {
                 const int pair = (L.get_info(s) >> 11) & 511;
 #pragma unroll
@@ -976,6 +1089,7 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
                             L.put(s, 1, make_double2(r1.x, __longlong_as_double(__double_as_longlong(r1.y) | (1ll << 20))));
                     }
                 }
+            }
             }
         }
     }
@@ -1409,7 +1523,11 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
                 const int pair = (int)(key[i] & 0x3ffu);
                 const uint32_t age = key[i] >> 12;
                 bool t = false;
-                for (int s = 0; s < n; ++s) t |= ((L.get_info(s) >> 11) & 511) == pair;
+                if constexpr (kHitMask<N>) {
+                    t = slot_of(pair) >= 0;
+                } else {
+                    for (int s = 0; s < n; ++s) t |= ((L.get_info(s) >> 11) & 511) == pair;
+                }
                 if (!t && age + 1 + xa < 3) {
                     FB_BOUND(L, w < (uint32_t)S::P, 6, w = S::P - 1);
                     L.cjn[(size_t)w * B + env] = jn[i];
@@ -1420,12 +1538,32 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
             }
         }
     }
-    for (int s = 0; s < n; ++s) {
+    auto put_entry = [&](long long info, double jn) {
         FB_BOUND(L, w < (uint32_t)S::P, 6, w = S::P - 1);
-        L.ckey[(size_t)w * B + env] = (uint16_t)(((L.get_info(s) >> 11) & 511) | (xa << 12));
+        L.ckey[(size_t)w * B + env] = (uint16_t)(((info >> 11) & 511) | (xa << 12));
         FB_BOUND(L, w < (uint32_t)S::P, 6, w = S::P - 1);
-        L.cjn[(size_t)w * B + env] = L.get_jn(s);
+        L.cjn[(size_t)w * B + env] = jn;
         ++w;
+    };
+    if constexpr (kHitMask<N>) {
+    const int nl = n < KLs ? n : KLs;
+    for (int s = 0; s < nl; ++s)
+        put_entry(__double_as_longlong(L.sh->rec[s][1][ln_].y), L.sh->rec[s][3][ln_].y);
+    // spill records: their info and jnAcc in batches of 8 independent loads (one round trip each)
+    for (int s0 = KLs; s0 < n; s0 += 8) {
+        double inf[8], jq[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int s = s0 + i < n ? s0 + i : n - 1;
+            inf[i] = *L.sp(s, 3);
+            jq[i] = *L.sp(s, 7);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            if (s0 + i < n) put_entry(__double_as_longlong(inf[i]), jq[i]);
+    }
+    } else {
+    for (int s = 0; s < n; ++s) put_entry(L.get_info(s), L.get_jn(s));
     }
     FB_BOUND(L, w <= (uint32_t)S::P, 2, w = S::P);
     e.meta.set_ncache(w);
