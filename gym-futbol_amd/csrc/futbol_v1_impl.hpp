@@ -304,6 +304,25 @@ __device__ __forceinline__ long long null_info()
     return pack_info(V1Shape<N>::Nb, 32, 0, false);
 }
 
+// element env of row k of a [rows][B] array, the scalar-base form (kScalarBase<N> below): the row's
+// base is wave-uniform (scalar registers) and the lane's part one 32-bit byte offset shared by every
+// row and field, so that the accesses take the saddr form of global_load / store instead of a 64-bit
+// vector address per row and field, which the kernels otherwise compute at the state loads and keep
+// live until the stores: 10v10 143.0 -> 137.2 us (scratch 756 -> 664 B per lane, PMC traffic 270 ->
+// 252 MB per launch), 7v7 -1.5%; 2v2 +2.7%, 5v5 +3.5%, 3v3 +0.5% (the bases then crowd the scalar
+// registers), so N <= 5 keep the plain indexing (at their call sites, verbatim: the N <= 5 code is
+// unchanged, and so are its ISA-gate results)
+#ifndef FUTBOL_SBASE_MIN
+#define FUTBOL_SBASE_MIN 6
+#endif
+template <int N>
+constexpr bool kScalarBase = N >= FUTBOL_SBASE_MIN;
+template <typename T>
+__device__ __forceinline__ T& soa(T* base, int k, int B, int env)
+{
+    return *reinterpret_cast<T*>(reinterpret_cast<char*>(base + (size_t)k * (size_t)B) + (uint32_t)env * (uint32_t)sizeof(T));
+}
+
 // global spill record (slot s >= K): 8 doubles [nx, ny, nMass, info, bias, -bounce, jBias, jnAcc]
 // (the LDS record's four double2 in order), at spill[env][s - K][f]: a record is one 64-byte line,
 // so the solve's per-sweep re-reads of an item's spill records stay in a few cache lines
@@ -533,10 +552,17 @@ __device__ __forceinline__ void load_cache_pre(const Lane<N, EPW>& L, uint32_t n
     static_assert(CKN<N> <= V1Shape<N>::P, "preloaded cache entries must lie inside the [P][B] arrays");
 #pragma unroll
     for (int c = 0; c < CKN<N>; ++c) {
+        if constexpr (kScalarBase<N>) {
+            const uint32_t k = soa(L.ckey, c, L.B, L.env);
+            const double j = soa(L.cjn, c, L.B, L.env);
+            ck[c] = (uint32_t)c < ncache ? k : 0xffffu;
+            cj[c] = (uint32_t)c < ncache ? j : 0.0;
+        } else {
         const uint32_t k = L.ckey[(size_t)c * L.B + L.env];
         const double j = L.cjn[(size_t)c * L.B + L.env];
         ck[c] = (uint32_t)c < ncache ? k : 0xffffu;
         cj[c] = (uint32_t)c < ncache ? j : 0.0;
+        }
     }
 }
 
@@ -1681,6 +1707,22 @@ constexpr bool kLateCache = N >= FUTBOL_LATE_CACHE_MIN;
 template <int N, bool BIAS = true>
 __device__ __forceinline__ void load_bodies(const V1Ptrs& st, int env, int B, Env<N>& e)
 {
+    if constexpr (kScalarBase<N>) {
+        sfor<V1Shape<N>::Nb>([&](auto K) {
+            constexpr int k = K;
+            const double2 p = soa(st.pxy, k, B, env), v = soa(st.vxy, k, B, env);
+            e.px[k] = p.x;
+            e.py[k] = p.y;
+            e.vx[k] = v.x;
+            e.vy[k] = v.y;
+            if constexpr (BIAS) {
+                const double2 vb = soa(st.bxy, k, B, env);
+                e.bx[k] = vb.x;
+                e.by[k] = vb.y;
+            }
+        });
+        return;
+    }
     sfor<V1Shape<N>::Nb>([&](auto K) {
         constexpr int k = K;
         const size_t o = (size_t)k * B + env;
@@ -1701,7 +1743,7 @@ __device__ __forceinline__ void load_bias(const V1Ptrs& st, int env, int B, Env<
 {
     sfor<V1Shape<N>::Nb>([&](auto K) {
         constexpr int k = K;
-        const double2 vb = st.bxy[(size_t)k * B + env];
+        const double2 vb = kScalarBase<N> ? soa(st.bxy, k, B, env) : st.bxy[(size_t)k * B + env];
         e.bx[k] = vb.x;
         e.by[k] = vb.y;
     });
@@ -1716,6 +1758,16 @@ __device__ __forceinline__ void load_env(const V1Ptrs& st, int env, int B, Env<N
 template <int N>
 __device__ __forceinline__ void store_env(const V1Ptrs& st, int env, int B, const Env<N>& e)
 {
+    if constexpr (kScalarBase<N>) {
+        sfor<V1Shape<N>::Nb>([&](auto K) {
+            constexpr int k = K;
+            soa(st.pxy, k, B, env) = make_double2(e.px[k], e.py[k]);
+            soa(st.vxy, k, B, env) = make_double2(e.vx[k], e.vy[k]);
+            soa(st.bxy, k, B, env) = make_double2(e.bx[k], e.by[k]);
+        });
+        soa(st.meta, 0, B, env) = e.meta.w;
+        return;
+    }
     sfor<V1Shape<N>::Nb>([&](auto K) {
         constexpr int k = K;
         const size_t o = (size_t)k * B + env;
@@ -1922,14 +1974,14 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
     const SegLds seg_g = fetch_seg(P);
     uint32_t araw[2 * N];
     if constexpr ((2 * N) % 4 == 0) {
-        const uint32_t* a32 = (const uint32_t*)(actions + (size_t)env * (2 * N));
+        const uint32_t* a32 = (const uint32_t*)(actions + (kScalarBase<N> ? (size_t)((uint32_t)env * (uint32_t)(2 * N)) : (size_t)env * (2 * N)));
         sfor<(2 * N) / 4>([&](auto W4) {
             constexpr int w = W4;
             const uint32_t x = a32[w];
             sfor<4>([&](auto Q) { araw[4 * w + Q] = (x >> (8 * Q)) & 0xffu; });
         });
     } else {
-        const uint16_t* a16 = (const uint16_t*)(actions + (size_t)env * (2 * N));
+        const uint16_t* a16 = (const uint16_t*)(actions + (kScalarBase<N> ? (size_t)((uint32_t)env * (uint32_t)(2 * N)) : (size_t)env * (2 * N)));
         sfor<N>([&](auto W2) {
             constexpr int w = W2;
             const uint32_t x = a16[w];
@@ -1938,12 +1990,12 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
         });
     }
     Env<N> e;
-    e.meta.w = st.meta[env];
+    e.meta.w = kScalarBase<N> ? soa(st.meta, 0, B, env) : st.meta[env];
     load_bodies<N, !kLateBias<N>>(st, env, B, e);
     uint32_t ck[CKN<N>];
     double cj[CKN<N>];
     if constexpr (!kLateCache<N>) load_cache_pre<N, EPW>(L, e.meta.ncache(), ck, cj);
-    const double ep_ret0 = st.ep_ret[env];
+    const double ep_ret0 = kScalarBase<N> ? soa(st.ep_ret, 0, B, env) : st.ep_ret[env];
     // lanes past B (last block) run the action phase on their shadow copy of env B-1 in
     // registers only (no store, no counter) and leave after the segment table is in LDS
     const double W = P.W, H = P.H;
@@ -2240,10 +2292,17 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
         FUTBOL_STAMP(ph == 0 ? 8 : 9);
     }
     FUTBOL_CRUMB(L, 80);
+    if constexpr (kScalarBase<N>) {
+        write_obs<N, OT>(e, obs + (size_t)((uint32_t)env * (uint32_t)(4 * S::Nb)));
+        soa(st.ep_ret, 0, B, env) = ret;
+        soa(reward, 0, B, env) = (OT)r;
+        soa(done_out, 0, B, env) = done ? 1 : 0;
+    } else {
     write_obs<N, OT>(e, obs + (size_t)env * (4 * S::Nb));
     st.ep_ret[env] = ret;
     reward[env] = (OT)r;
     done_out[env] = done ? 1 : 0;
+    }
     store_env<N>(st, env, B, e);
     // The clamped-action count (futbol_invalid_actions) is the step's last memory operation, where no
     // value is live.  It used to follow the action decode, amid ~60 loads in flight and every state
