@@ -84,7 +84,7 @@ def _rounds(lens, A=64):
     return sum(max(lens[i:i + A]) for i in range(0, len(lens), A)) if lens else 0
 
 
-def strategies(comps_per_env, A=64):
+def strategies(comps_per_env, A=64, spill_k=4):
     """comps_per_env: per env of one wave, the list of its components' record counts.  The wave's solve
     cost in record-units (rounds of A items, each round as long as its longest item):
       whole:     one item per env and half, in env order (today's N >= 4 solve);
@@ -111,7 +111,9 @@ def strategies(comps_per_env, A=64):
     return (_rounds(items_whole, A), _rounds(items_comp, A), _rounds(sorted(items_comp, reverse=True), A), best,
             _rounds(items_b, A), rounds_global, _rounds(sorted(items_whole, reverse=True), A),
             max(items_comp, default=0) if len(items_comp) <= A else rounds_global,  # today's N <= 3 rule
-            max(items_comp, default=0) if len(items_comp) <= A else _rounds(sorted(items_whole, reverse=True), A))
+            max(items_comp, default=0) if len(items_comp) <= A else _rounds(sorted(items_whole, reverse=True), A),
+            _rounds(sorted([x for c in comps_per_env if c for x in (c if sum(c) > spill_k else [sum(c)])
+                            for _ in (0, 1)], reverse=True), A))
 
 
 def main():
@@ -132,7 +134,7 @@ def main():
     W = B // 64
     whole_w, comp_w, items_w, spill_w = [], [], [], []
     strat = {"whole": [], "comp": [], "comp_sort": [], "split": [], "comp_bucket4": [], "whole_globalm": [],
-             "whole_sorted": [], "n23_today": [], "n23_fallback_sorted": []}
+             "whole_sorted": [], "n23_today": [], "n23_fallback_sorted": [], "spill_envs_split_sorted": []}
     K = a.lds_slots if a.lds_slots is not None else 4
     for t in range(a.steps):
         ora.step(rng.integers(0, 5, (B, 2 * n), dtype=np.int32), nthreads=a.threads)
@@ -145,9 +147,9 @@ def main():
             rows = []
             for w in range(W):
                 pc_ = percomp[64 * w:64 * w + 64]
-                rows.append(strategies([list(x[x > 0]) for x in pc_]))
+                rows.append(strategies([list(x[x > 0]) for x in pc_], spill_k=K))
             for k_, v_ in zip(("whole", "comp", "comp_sort", "split", "comp_bucket4", "whole_globalm", "whole_sorted",
-                               "n23_today", "n23_fallback_sorted"),
+                               "n23_today", "n23_fallback_sorted", "spill_envs_split_sorted"),
                               np.array(rows).T):
                 strat[k_].append(v_)
         if a.lds_slots is not None:
