@@ -292,7 +292,13 @@ def stamps_report(venv, one_step, args):
            "phases": dict([(STAMP_SLOTS[i], {"cycles": per[i], "share": per[i] / tot}) for i in range(11)] +
                           [(SUB_SLOTS[k], {"cycles": per[k], "share": per[k] / tot}) for k in SUB_SLOTS]),
            "solver_records_per_wave_step": per[15],
-           "segment_candidate_iterations_per_wave_step": per[24], "segment_contact_iterations_per_wave_step": per[25]}
+           "segment_candidate_iterations_per_wave_step": per[24], "segment_contact_iterations_per_wave_step": per[25],
+           # FUTBOL_STAT slots (space_step phase 0): contact work-list hits per wave-step, the fraction of
+           # wave-steps whose hits overflow the work-list table (every lane computes its own contacts),
+           # with a lane past the preloaded cache entries, with spill records; out-of-bounds, goals
+           "worklist_hits_per_wave_step": per[26], "worklist_overflow_wave_frac": per[27],
+           "cache_past_preload_wave_frac": per[28], "spill_wave_frac": per[29],
+           "out_of_bounds_per_wave_step": per[30], "goals_per_wave_step": per[31]}
     # single-launch snapshots: wave start/end (100 MHz realtime), cycles, placement
     snaps = []
     waves = []  # per-wave slots of every snapshot launch (tail study: --stamps-dump)
