@@ -45,11 +45,12 @@ constexpr double kPlayerR = 1.5, kBallR = 1.0, kSegR = 1.0;
 constexpr double kPlayerMinv = 1.0 / 20.0, kBallMinv = 1.0 / 10.0;
 constexpr double kPlayerVmax = 10.0, kBallVmax = 25.0;
 constexpr double kE = 0.2;  // elasticity of players and ball; segments 0
-// arbiter-cache entries preloaded into registers: FUTBOL_CK_SMALL (6) for N < 5, FUTBOL_CK_LARGE (8) for every
-// N >= 5 (5v5 and 10v10 envs hold more cached arbiters: a lane with more than CKN entries sends
-// its whole wave through the global lookup loops)
+// arbiter-cache entries preloaded into registers: FUTBOL_CK_SMALL (6) for N < 5, FUTBOL_CK_LARGE (4) for
+// N = 5 (a lane with more than CKN entries sends its whole wave through the batched lookup loops; 8
+// until round 5, when the hit-mask lookups made those loops cheap for 5v5: 8 -> 4 entries, 50.1 ->
+// 49.3 us; 3 equal, 2 and 6 no gain)
 #ifndef FUTBOL_CK_LARGE
-#define FUTBOL_CK_LARGE 8
+#define FUTBOL_CK_LARGE 4
 #endif
 #ifndef FUTBOL_CK_SMALL
 #define FUTBOL_CK_SMALL 6
