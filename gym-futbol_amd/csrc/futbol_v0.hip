@@ -144,9 +144,14 @@ __device__ __forceinline__ int defence_near(const Ctx& c, const Env& e)
 }
 
 // _set_vector_observation (:300-530)
+// pre_mag >= 0: |ball - agent| of the step's initial state (the step's first batch of squares), valid
+// while the ball is where it was then (the agents' positions do not change before the physics): the
+// non-holder's get_vec then reuses it instead of squaring again -- the same squares of the same
+// differences, so the same magnitude, and one slow glibc round less per agent in most waves
 template <int a>
 __device__ __forceinline__ void set_vector_observation(const Ctx& c, Env& e, bool has_ball, int action,
-                                                       bool set_target, double tgx, double tgy)
+                                                       bool set_target, double tgx, double tgy,
+                                                       double pre_mag = -1.0, double pbx = 0.0, double pby = 0.0)
 {
     constexpr bool right = a >= 2;
     const V0Params* P = c.P;
@@ -218,7 +223,13 @@ __device__ __forceinline__ void set_vector_observation(const Ctx& c, Env& e, boo
         }
     } else {
         double btax, btay, gtax, gtay;
-        const double btam = get_vec(ball[0], ball[1], ag[0], ag[1], btax, btay);
+        double btam;
+        if (pre_mag >= 0.0 && ball[0] == pbx && ball[1] == pby) {
+            vec_only(ball[0], ball[1], ag[0], ag[1], btax, btay);
+            btam = pre_mag;
+        } else {
+            btam = get_vec(ball[0], ball[1], ag[0], ag[1], btax, btay);
+        }
         vec_only(right ? 0.0 : P->length, P->width / 2, ag[0], ag[1], gtax, gtay);
         if (action == INTERCEPT) {
             const bool success = Stream::uniform01_of(blk[1]) < intercept_chance(btam);
@@ -305,7 +316,8 @@ __device__ __forceinline__ void resolve_shot(Env& e, const Stream& rs)
 
 // _opp_team_set_vector_observation (:864-983); m3 = |ball - opp_1|, |ball - opp_2|, |opp_2 - opp_1|
 // (= |opp_1 - opp_2|: pow(-x, 2) = pow(x, 2)) of the state at the top of the step
-__device__ __forceinline__ void opp_team(const Ctx& c, Env& e, const double (&m3)[3])
+__device__ __forceinline__ void opp_team(const Ctx& c, Env& e, const double (&m3)[3], double bx0, double by0,
+                                         double bvx0, double bvy0, double bvmag0)
 {
     const V0Params* P = c.P;
     const bool o1has = e.owner == OPP_1, o2has = e.owner == OPP_2;
@@ -335,14 +347,17 @@ __device__ __forceinline__ void opp_team(const Ctx& c, Env& e, const double (&m3
             else { a2 = RUN; s2 = true; vec_only(dpx, dpy, o2[0], o2[1], t2x, t2y); }
         }
     }
-    set_vector_observation<OPP_1>(c, e, o1has, a1, s1, t1x, t1y);
-    set_vector_observation<OPP_2>(c, e, o2has, a2, s2, t2x, t2y);
+    set_vector_observation<OPP_1>(c, e, o1has, a1, s1, t1x, t1y, m3[0], bx0, by0);
+    set_vector_observation<OPP_2>(c, e, o2has, a2, s2, t2x, t2y, m3[1], bx0, by0);
     if (e.owner == NOONE && opp1_action == RUN && opp2_action == RUN) {
         // anticipate the ball (:962-982)
         double nb[5];
 #pragma unroll
         for (int f = 0; f < 5; ++f) nb[f] = e.r[BALL][f];
-        step_by_observation(nb);
+        // (no opponent touched the ball: its velocity is the step's initial one, whose magnitude the
+        // first batch of squares computed)
+        if (nb[2] == bvx0 && nb[3] == bvy0) step_by_observation_mag(nb, bvmag0);
+        else step_by_observation(nb);
         const double v1x = nb[0] - o1[0], v1y = nb[1] - o1[1], v2x = nb[0] - o2[0], v2y = nb[1] - o2[1];
         double m1, m2;
         get_mag2(nb[0], nb[1], o1[0], o1[1], nb[0], nb[1], o2[0], o2[1], m1, m2);
@@ -538,18 +553,20 @@ __device__ __forceinline__ void v0_step_body(const V0Params* __restrict__ P, con
     // the magnitudes of the step's initial state, their squares in one batch: _get_reward's ball to
     // ai_1 / ai_2 (of the copies o_b, o_ai_1, o_ai_2) and the opponents' get_action_type (hard-coded
     // opponent: ball to opp_1 / opp_2, opp_1 to opp_2)
-    double b2a1, b2a2, m3[3];
+    double b2a1, b2a2, m3[3], bvmag0 = 0.0;
     {
         const double* o1 = e.r[OPP_1];
         const double* o2 = e.r[OPP_2];
-        const double d[10] = {ob[0] - oa1[0], ob[1] - oa1[1], ob[0] - oa2[0], ob[1] - oa2[1],
-                              ob[0] - o1[0], ob[1] - o1[1], ob[0] - o2[0], ob[1] - o2[1], o2[0] - o1[0], o2[1] - o1[1]};
-        double q[10];
+        const double d[12] = {ob[0] - oa1[0], ob[1] - oa1[1], ob[0] - oa2[0], ob[1] - oa2[1],
+                              ob[0] - o1[0], ob[1] - o1[1], ob[0] - o2[0], ob[1] - o2[1], o2[0] - o1[0], o2[1] - o1[1],
+                              ob[2], ob[3]};
+        double q[12];
         if (P->random_opp) {
             glibc_pow2_batch<4>(*reinterpret_cast<const double(*)[4]>(d), *reinterpret_cast<double(*)[4]>(q),
                                 s_pow_log, s_pow_exp);
         } else {
-            glibc_pow2_batch<10>(d, q, s_pow_log, s_pow_exp);
+            glibc_pow2_batch<12>(d, q, s_pow_log, s_pow_exp);
+            bvmag0 = sqrt(q[10] + q[11]);
             m3[0] = sqrt(q[4] + q[5]);
             m3[1] = sqrt(q[6] + q[7]);
             m3[2] = sqrt(q[8] + q[9]);
@@ -562,10 +579,10 @@ __device__ __forceinline__ void v0_step_body(const V0Params* __restrict__ P, con
         set_vector_observation<OPP_1>(c, e, e.owner == OPP_1, t / 4, false, 0, 0);
         set_vector_observation<OPP_2>(c, e, e.owner == OPP_2, t % 4, false, 0, 0);
     } else {
-        opp_team(c, e, m3);
+        opp_team(c, e, m3, ob[0], ob[1], ob[2], ob[3], bvmag0);
     }
-    set_vector_observation<AI_1>(c, e, e.owner == AI_1, a0, false, 0, 0);
-    set_vector_observation<AI_2>(c, e, e.owner == AI_2, a1, false, 0, 0);
+    set_vector_observation<AI_1>(c, e, e.owner == AI_1, a0, false, 0, 0, b2a1, ob[0], ob[1]);
+    set_vector_observation<AI_2>(c, e, e.owner == AI_2, a1, false, 0, 0, b2a2, ob[0], ob[1]);
     resolve_shot(e, rs);
     {   // _step_vector_observations + the ball's _step_by_observation: the five magnitudes are
         // independent, so their squares go through one glibc_pow2_batch
