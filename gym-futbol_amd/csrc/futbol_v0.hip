@@ -151,7 +151,8 @@ __device__ __forceinline__ int defence_near(const Ctx& c, const Env& e)
 template <int a>
 __device__ __forceinline__ void set_vector_observation(const Ctx& c, Env& e, bool has_ball, int action,
                                                        bool set_target, double tgx, double tgy,
-                                                       double pre_mag = -1.0, double pbx = 0.0, double pby = 0.0)
+                                                       double pre_mag = -1.0, double pbx = 0.0, double pby = 0.0,
+                                                       double mate_pre = -1.0)
 {
     constexpr bool right = a >= 2;
     const V0Params* P = c.P;
@@ -209,7 +210,15 @@ __device__ __forceinline__ void set_vector_observation(const Ctx& c, Env& e, boo
         } else {  // ASSIST
             const double* mate = e.r[MATE[a]];
             double vx, vy;
-            const double mag = get_vec(mate[0], mate[1], ball[0], ball[1], vx, vy);
+            double mag;
+            // |mate - ball| = |ball - mate| of the first batch while the ball has not moved
+            // (mate - ball = -(ball - mate) exactly, and pow(-x, 2) = pow(x, 2))
+            if (mate_pre >= 0.0 && ball[0] == pbx && ball[1] == pby) {
+                vec_only(mate[0], mate[1], ball[0], ball[1], vx, vy);
+                mag = mate_pre;
+            } else {
+                mag = get_vec(mate[0], mate[1], ball[0], ball[1], vx, vy);
+            }
             double cps = mag / STEP_SIZE;
             if (cps > SHOOT_SPEED) cps = SHOOT_SPEED;
             ball[4] = Stream::uniform_of(blk[1], cps - 1, cps + 1);
@@ -347,8 +356,8 @@ __device__ __forceinline__ void opp_team(const Ctx& c, Env& e, const double (&m3
             else { a2 = RUN; s2 = true; vec_only(dpx, dpy, o2[0], o2[1], t2x, t2y); }
         }
     }
-    set_vector_observation<OPP_1>(c, e, o1has, a1, s1, t1x, t1y, m3[0], bx0, by0);
-    set_vector_observation<OPP_2>(c, e, o2has, a2, s2, t2x, t2y, m3[1], bx0, by0);
+    set_vector_observation<OPP_1>(c, e, o1has, a1, s1, t1x, t1y, m3[0], bx0, by0, m3[1]);
+    set_vector_observation<OPP_2>(c, e, o2has, a2, s2, t2x, t2y, m3[1], bx0, by0, m3[0]);
     if (e.owner == NOONE && opp1_action == RUN && opp2_action == RUN) {
         // anticipate the ball (:962-982)
         double nb[5];
@@ -581,8 +590,8 @@ __device__ __forceinline__ void v0_step_body(const V0Params* __restrict__ P, con
     } else {
         opp_team(c, e, m3, ob[0], ob[1], ob[2], ob[3], bvmag0);
     }
-    set_vector_observation<AI_1>(c, e, e.owner == AI_1, a0, false, 0, 0, b2a1, ob[0], ob[1]);
-    set_vector_observation<AI_2>(c, e, e.owner == AI_2, a1, false, 0, 0, b2a2, ob[0], ob[1]);
+    set_vector_observation<AI_1>(c, e, e.owner == AI_1, a0, false, 0, 0, b2a1, ob[0], ob[1], b2a2);
+    set_vector_observation<AI_2>(c, e, e.owner == AI_2, a1, false, 0, 0, b2a2, ob[0], ob[1], b2a1);
     resolve_shot(e, rs);
     {   // _step_vector_observations + the ball's _step_by_observation: the five magnitudes are
         // independent, so their squares go through one glibc_pow2_batch
