@@ -92,8 +92,14 @@ def _sched_flags(src):
     return ["-mllvm", "-amdgpu-sched-strategy=" + SCHED]
 # A/B of compiler options: FUTBOL_EXTRA_CFLAGS="..." (with a FUTBOL_BUILD_VARIANT name)
 CFLAGS += os.environ.get("FUTBOL_EXTRA_CFLAGS", "").split()
-# (a variant name's "_"-separated words select these, e.g. FUTBOL_BUILD_VARIANT=kx6_bounds)
-_VWORDS = set(VARIANT.split("_"))
+# Diagnostic defines, selected explicitly: a variant named exactly "stamps" / "crumbs" / "bounds", or a
+# "_"-separated word with a "+" prefix (e.g. FUTBOL_BUILD_VARIANT=kx6_+bounds), so that a plain word of an
+# A/B variant's name (e.g. "no_stamps") never turns a diagnostic on
+_DIAG_WORDS = ("stamps", "crumbs", "bounds")
+_VWORDS = {VARIANT} & set(_DIAG_WORDS) | {w[1:] for w in VARIANT.split("_") if w.startswith("+")}
+_unknown = _VWORDS - set(_DIAG_WORDS)
+if _unknown:
+    raise SystemExit("FUTBOL_BUILD_VARIANT=%s: unknown diagnostic word(s) %s" % (VARIANT, sorted(_unknown)))
 if "stamps" in _VWORDS:
     CFLAGS.append("-DFUTBOL_STAMPS")
 if "crumbs" in _VWORDS:  # diagnostic: per-wave phase markers in host-coherent memory
@@ -202,6 +208,12 @@ def build(force=False, jobs=None, verbose=True):
             obj = os.path.join(PRODUCT_OBJ, os.path.basename(src) + ".o")
             if not os.path.exists(obj):
                 raise RuntimeError("FUTBOL_VARIANT_TUS: build the product first (%s missing)" % obj)
+            # the product object must be current with the product sources, or the A/B would link stale code
+            psrc = os.path.join(HERE, "csrc", os.path.basename(src))
+            pdeps = (glob.glob(os.path.join(HERE, "csrc", "*.hpp")) + glob.glob(os.path.join(HERE, "csrc", "*.h")) +
+                     [os.path.join(ROOT, "include", "futbol.h")])
+            if _stale(obj, [psrc] + pdeps):
+                raise RuntimeError("FUTBOL_VARIANT_TUS: %s is older than the product sources; rebuild the product" % obj)
             return obj
         return _compile(src, force)
     with ThreadPoolExecutor(jobs) as ex:

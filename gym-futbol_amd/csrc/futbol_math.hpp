@@ -164,7 +164,8 @@ __host__ __device__ inline void cr_sincos(double a, double* sn, double* cs)
 // directions are bit-identical to the reference's (oracle/oracle_math.h holds the checker's own
 // restatement, tests/test_glibc_sincos.py pins it against the host libm).  |x| < 105414350 only
 // (screw_vec's angles are below 4.5 in magnitude); beyond, the correctly rounded cr_sincos.
-static constexpr double kSinCosTab[440] = {FUTBOL_SINCOSTAB_ROWS};
+// (16-byte aligned: the v0 step kernel copies it into LDS in 16-byte LDS-DMA pieces, futbol_v0.hip)
+alignas(16) static constexpr double kSinCosTab[440] = {FUTBOL_SINCOSTAB_ROWS};
 
 namespace glibc_sincos {
 constexpr double BIG = 0x1.8p45, SN3 = -0x1.5555555555515p-3, SN5 = 0x1.11110e829872fp-7;

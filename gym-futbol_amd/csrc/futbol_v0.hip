@@ -63,6 +63,8 @@ __device__ __forceinline__ void stage_pow_tables()
     char* ds = reinterpret_cast<char*>(s_sincos);
     static_assert(sizeof(s_pow_log) == 3 * 1024 && sizeof(s_pow_exp) == 2 * 1024 && sizeof(s_sincos) == 3 * 1024 + 448,
                   "DMA pieces");
+    static_assert(__alignof__(kSinCosTab) >= 16 && __alignof__(kPowLog) >= 16 && __alignof__(kPowExp) >= 16,
+                  "16-byte LDS-DMA pieces need 16-byte aligned sources");
 #pragma unroll
     for (int j = 0; j < 3; ++j) __builtin_amdgcn_global_load_lds(pl + 64 * j + lane, (lds_void*)(dl + 1024 * j), 16, 0, 0);
 #pragma unroll

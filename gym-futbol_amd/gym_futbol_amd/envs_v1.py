@@ -4,7 +4,8 @@ Mirrors gym_futbol/envs_v1/futbol_env.py:62-515 (`Futbol`): same constructor
 kwargs, `reset()`, `step(left_player_action) -> (obs, reward, done, {})`,
 `random_action()`, `action_space`, `observation_space`, and the attributes the
 reference's notebook reads (`width`, `height`, `number_of_player`,
-`current_time`, `ball_owner_side`).  The step runs on the GPU (a B = 1
+`current_time`, `ball_owner_side`, and `space` for its drawing cells'
+`env.space.debug_draw(pymunk.matplotlib_util.DrawOptions(ax))`).  The step runs on the GPU (a B = 1
 context, fp64 outputs, no auto-reset: like the reference, `done` stays True if
 one keeps stepping).  For throughput use FutbolVecEnv / make(..., num_envs=B).
 """
@@ -65,6 +66,14 @@ class Futbol:
         s = self._venv.get_state()
         return np.stack([s["px"], s["py"]], 1), np.stack([s["vx"], s["vy"]], 1)
 
+    @property
+    def space(self):
+        """Stand-in for the reference's pymunk Space (futbol_env.py:75) as far as the notebook uses it:
+        `space.debug_draw(options)` (colab_notebook.ipynb:289,616) draws the field into `options.ax`
+        (pymunk.matplotlib_util.DrawOptions keeps its Axes there).  There is no pymunk Space here: the
+        physics is the GPU kernel."""
+        return FieldSpace(self.width, self.height, self.number_of_player, lambda: self.body_states()[0])
+
     def render(self, ax=None):
         """Matplotlib drawing of the field (replaces pymunk's debug_draw, futbol_env.py:236-243)."""
         import matplotlib.pyplot as plt
@@ -78,6 +87,23 @@ class Futbol:
 
     def close(self):
         self._venv.close()
+
+
+class FieldSpace:
+    """`Futbol.space`: the part of pymunk's Space API the reference's notebook calls.  `positions` returns
+    the current body positions [Nb, 2] (A0.., B0.., ball)."""
+
+    def __init__(self, width, height, n, positions):
+        self.width, self.height, self.number_of_player = width, height, n
+        self._positions = positions
+
+    def debug_draw(self, options):
+        """pymunk Space.debug_draw (futbol_env.py:236-243 via the notebook): draw into options.ax, or into
+        `options` itself when it is a matplotlib Axes."""
+        ax = getattr(options, "ax", options)
+        if not hasattr(ax, "add_patch"):
+            raise TypeError("debug_draw needs pymunk.matplotlib_util.DrawOptions(ax) or an Axes, got %r" % (options,))
+        return draw_field(ax, self.width, self.height, np.asarray(self._positions()), self.number_of_player)
 
 
 def field_segments(width, height, goal_size=20):

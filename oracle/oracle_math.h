@@ -8,15 +8,18 @@
  *                         CPython/numpy on this glibc.  Pinned bit-for-bit against
  *                         the reference's own outputs (tests/golden/).
  *
- *  liboracle_portable.so  (-DORACLE_PORTABLE) squares with `*` and uses the
- *                         correctly rounded double-double sin/cos below, i.e. the
- *                         arithmetic the HIP kernels use (glibc's pow is not
- *                         correctly rounded: pow(x,2) != x*x for ~0.08% of
- *                         doubles, and neither are its sin/cos; neither can be
- *                         reproduced on the GPU).  The
- *                         kernels are compared against this build bit-for-bit;
- *                         this build is compared against the faithful one with a
- *                         tolerance (tests/test_oracle_modes.py).
+ *  liboracle_portable.so  (-DORACLE_PORTABLE) the arithmetic the HIP kernels use,
+ *                         written without calls into the host libm: glibc's
+ *                         pow(x, 2.0) and sin / cos restated operation for
+ *                         operation (orc_glibc_pow2 / orc_glibc_sin / _cos below:
+ *                         glibc's pow is not correctly rounded -- pow(x,2) != x*x
+ *                         for ~0.08% of doubles -- and neither are its sin/cos) for
+ *                         every v0 square and sin/cos and for the envs_v1 squares
+ *                         that feed the state; only the envs_v1 reward's squares
+ *                         are x*x (ORC_SQ_V1).  The kernels are compared against
+ *                         this build bit-for-bit; this build against the faithful
+ *                         one in tests/test_oracle_modes.py (observations
+ *                         bit-identical; reward bits differ by <= 2.3e-13).
  *
  * The tape's normal draw uses the +,-,*,/-only orc_pm_log / orc_pm_sincos in BOTH
  * builds (and in tests/rng_tape.py): it is part of the tape contract.

@@ -64,6 +64,21 @@ def test_futbol_facade_matches_oracle():
         f.step([5] + [0] * 9)
     with pytest.raises(ValueError):
         f.step([0] * 4)
+    # the notebook's drawing cells (colab_notebook.ipynb:288-289): env.space.debug_draw(DrawOptions(ax))
+    import matplotlib
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+
+    class _DrawOptions:
+        def __init__(self, ax):
+            self.ax = ax
+
+    ax = plt.axes(xlim=(-5, f.width + 5), ylim=(-5, f.height + 5))
+    f.space.debug_draw(_DrawOptions(ax))
+    pos, _ = f.body_states()
+    assert len(ax.get_lines()) == 12 and len(ax.patches) == 11
+    assert np.allclose([c.center for c in ax.patches], pos)
+    plt.close("all")
     f.close()
 
 

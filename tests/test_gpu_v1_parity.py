@@ -1,7 +1,8 @@
 """envs_v1 kernel vs the CPU oracle, on the GPU.
 
 The kernel is compared BIT-FOR-BIT with oracle/liboracle_portable.so (the
-oracle with x*x squares, i.e. the kernel's arithmetic; see oracle/oracle_math.h):
+oracle with the kernels' arithmetic: glibc's pow(x, 2) restated for the squares
+that feed the state, x*x only for the reward's; see oracle/oracle_math.h):
 obs, reward, done, every body's p / v / v_bias and the arbiter cache, at every
 step of free-running rollouts with auto-reset, and on teacher-forced crowded
 states that exercise multi-contact solves, cached-impulse warm starts and the
@@ -90,6 +91,7 @@ def _crowded_states(n, B, seed):
     """Oracle envs in random crowded configurations: bodies overlapping each other
     and the walls / goal boxes, random v, v_bias and random cached arbiters."""
     rng = np.random.default_rng(seed)
+    lay = _layout(n)
     ora = O.V1Vec(B, N=n, seed=seed, portable=True)
     nb = 2 * n + 1
     P = nb * 12 + nb * (nb - 1) // 2
@@ -111,11 +113,11 @@ def _crowded_states(n, B, seed):
         e.stamp = 50
         e.curr_dt = [0.1, 0.0001][int(rng.random() < 0.2)]
         e.current_time = 0.0
-        # up to 18 / 24 cached arbiters (N < 5 / N >= 5): more than the kernel's register-preloaded
-        # entries plus one batched read (futbol_solver_layout), so that the lookups and the in-place
-        # compaction past the preloaded entries run on the first step
-        ckn = 8 if n >= 5 else 6
-        for p in rng.choice(P, size=int(rng.integers(0, 3 * ckn + 1)), replace=False):
+        # up to 3x (the kernel's register-preloaded entries + one batched read) cached arbiters, sized
+        # from the loaded library's own layout (futbol_solver_layout), so that the lookups and the
+        # in-place compaction past the preloaded entries run on the first step
+        ckn = lay["cache_preload"] + lay["cache_batch"]
+        for p in rng.choice(P, size=int(rng.integers(0, min(P, 3 * ckn) + 1)), replace=False):
             p = int(p)
             age = int(rng.integers(0, 3))
             e.arb_exists[p] = 1

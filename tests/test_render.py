@@ -59,3 +59,31 @@ def test_observation_from_state_matches_oracle():
                 st[f][k * B + i] = getattr(ora.envs[i], f)[k]
     for i in range(B):
         assert np.array_equal(observation_from_state(st, n, i), obs[i])
+
+
+class _DrawOptions:
+    """the one attribute of pymunk.matplotlib_util.DrawOptions that debug_draw needs"""
+
+    def __init__(self, ax):
+        self.ax = ax
+
+
+def test_space_debug_draw_stub_options():
+    """colab_notebook.ipynb:288-289,615-616: env.space.debug_draw(DrawOptions(ax)) -- here on a CPU
+    FieldSpace over the oracle's formation positions (tests/test_gpu_api.py runs it on Futbol)."""
+    from gym_futbol_amd.envs_v1 import FieldSpace
+    n = 2
+    e = O.OrcV1()
+    O.lib().orc_v1_init(C.byref(e), n, 105.0, 68.0, 30.0, 0, 0)
+    nb = 2 * n + 1
+    pos = np.stack([np.frombuffer(e.px, np.float64)[:nb], np.frombuffer(e.py, np.float64)[:nb]], 1)
+    space = FieldSpace(105.0, 68.0, n, lambda: pos)
+    fig = plt.figure()
+    ax = plt.axes(xlim=(-5, 110), ylim=(-5, 73))
+    ax.set_aspect("equal")
+    space.debug_draw(_DrawOptions(ax))
+    assert len(ax.get_lines()) == 12 and len(ax.patches) == nb
+    assert np.allclose([c.center for c in ax.patches], pos)
+    with pytest.raises(TypeError):
+        space.debug_draw(object())
+    plt.close(fig)
