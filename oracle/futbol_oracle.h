@@ -52,6 +52,8 @@ typedef struct {
     int32_t arb_inlist[ORC_MAXP];               /* in last cpSpaceStep's arbiter list */
     double arb_jn[ORC_MAXP];                    /* jnAcc of its (single) contact */
     uint32_t n_out, n_goal;                     /* diagnostics: out-of-bounds fixes, goals so far */
+    int32_t last_out_wall, last_out_pick;       /* diagnostics: the last step's out-of-bounds wall (-1: none) and
+                                                   restarted player (tests/test_gpu_v1_parity.py covers every leaf) */
 } OrcV1;
 
 /* v0 (gym_futbol/envs/futbol_env.py) */

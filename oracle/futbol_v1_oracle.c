@@ -502,6 +502,8 @@ static int check_and_fix_out_bounds(OrcV1 *e, OracleRng *g)
     const int ball = 2 * e->N;
     int w = -1;
     for (int s = 0; s < 6; ++s) if (ball_touches_seg(e, s)) { w = s; break; }
+    e->last_out_wall = w;
+    e->last_out_pick = -1;
     if (w < 0) return 0;
     double bx = e->px[ball], by = e->py[ball];
     double dbx = 0, dby = 0, dpx = 0, dpy = 0;
@@ -516,6 +518,7 @@ static int check_and_fix_out_bounds(OrcV1 *e, OracleRng *g)
     else { pick = e->N + oracle_choice(g, e->N); e->owner = 1; }
     e->px[pick] = bx + dpx; e->py[pick] = by + dpy;
     e->vx[pick] = 0.0; e->vy[pick] = 0.0;
+    e->last_out_pick = pick;
     return 1;
 }
 

@@ -27,7 +27,8 @@ class OrcV1(C.Structure):
                 ("stamp", C.c_uint32), ("curr_dt", C.c_double),
                 ("arb_exists", C.c_int32 * MAXP), ("arb_stamp", C.c_uint32 * MAXP),
                 ("arb_state", C.c_int32 * MAXP), ("arb_inlist", C.c_int32 * MAXP),
-                ("arb_jn", C.c_double * MAXP), ("n_out", C.c_uint32), ("n_goal", C.c_uint32)]
+                ("arb_jn", C.c_double * MAXP), ("n_out", C.c_uint32), ("n_goal", C.c_uint32),
+                ("last_out_wall", C.c_int32), ("last_out_pick", C.c_int32)]
 
 
 class OrcV0(C.Structure):

@@ -53,6 +53,33 @@ def disassemble(path, arch="gfx950"):
                                text=True, check=True).stdout for co in code_objects(path, tmp, arch)]
 
 
+def long_branch(ins, i):
+    """A relaxed long branch ending at ins[i] (past the SOPP branches' 16-bit range, big kernels):
+    s_getpc_b64 s[x:x+1]; s_add_u32 sx, sx, lo; s_addc_u32 sx+1, sx+1, hi; s_setpc_b64 s[x:x+1] jumps to
+    (address of s_getpc) + 4 + (hi:lo).  ins: [(address, text)].  Returns (target, relaxed_execz): the
+    second is True when the sequence is the taken side of a relaxed s_cbranch_execz (an s_cbranch_execnz
+    right before it skips over it).  None when ins[i] is not such a sequence."""
+    m = re.match(r"^s_setpc_b64 s\[(\d+):(\d+)\]$", ins[i][1])
+    if not m or i < 3:
+        return None
+    x = int(m.group(1))
+    (ga, gt), ad, ac = ins[i - 3], ins[i - 2][1], ins[i - 1][1]
+    ma = re.match(r"^s_add_u32 s(\d+), s(\d+), (0x[0-9a-f]+|-?\d+)$", ad)
+    mc = re.match(r"^s_addc_u32 s(\d+), s(\d+), (0x[0-9a-f]+|-?\d+)$", ac)
+    if gt != "s_getpc_b64 s[%d:%d]" % (x, x + 1) or not (ma and mc):
+        return None
+    if not (int(ma.group(1)) == x == int(ma.group(2)) and int(mc.group(1)) == x + 1 == int(mc.group(2))):
+        return None
+    off = ((int(mc.group(3), 0) & 0xffffffff) << 32) | (int(ma.group(3), 0) & 0xffffffff)
+    if off >= 1 << 63:
+        off -= 1 << 64
+    execz = False
+    if i >= 4 and ins[i - 4][1].startswith("s_cbranch_execnz"):
+        o = int(ins[i - 4][1].split()[1])
+        execz = ins[i - 4][0] + 4 + 4 * (o - 65536 if o >= 32768 else o) == ins[i][0] + 4
+    return ga + 4 + off, execz
+
+
 def scan(disasm):
     """findings of one llvm-objdump -d listing"""
     cur = None
@@ -67,7 +94,17 @@ def scan(disasm):
             ins.append((int(m.group(2), 16), cur, m.group(1)))
     index = {a: i for i, (a, _, _) in enumerate(ins)}
     starts, execz = set(), set()
-    for a, k, t in ins:
+    pairs = [(a, re.sub(r"\s+", " ", t)) for a, _, t in ins]
+    for i, (a, k, t) in enumerate(ins):
+        if t.startswith("s_setpc_b64"):
+            # a relaxed long branch: a block start, and the join of a skipped branch when it is the taken
+            # side of a relaxed s_cbranch_execz (kernels past 128 KB of code: N >= 8)
+            lb = long_branch(pairs, i)
+            if lb is not None:
+                starts.add(lb[0])
+                if lb[1]:
+                    execz.add(lb[0])
+            continue
         if t.startswith(("s_cbranch", "s_branch")):
             # SOPP branch: target = address + 4 + 4 * simm16
             off = int(t.split()[1])

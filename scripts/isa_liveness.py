@@ -27,15 +27,19 @@ encoding is partial: DPP / SDWA / op_sel / d16 / v_writelane / MAC-style tied de
 use + def.  The product build's objects have no finding; the kx6 and latec builds' failing objects do
 (DESIGN.md section 6).
 
-The gate (gym-futbol_amd/build.py) judges LOADED values (global / LDS loads; a scratch reload is a
-copy): a load's result that is only copied and lost cannot be dead code -- LLVM deletes unused loads --
-and both round-4 faults are of this kind.  `--all` also lists arithmetic results that are only copied
-and lost: the shipped N = 9 instances have 25 such v_add_f64 per affected kernel (the out-of-bounds
-restart's new player position, bx0 + dpx, computed once before the pick switch and again in every
-leaf; the first copy is never read), bit-exact on the GPU at 2 048 envs x 320 steps in every
-instance -- dead code left after register allocation, so not a gate criterion.
+The gate (gym-futbol_amd/build.py) runs with `--all`: LOADED values (global / LDS loads; a scratch reload
+is a copy) and computed ones.  A result that is only copied and lost cannot be dead code -- LLVM deletes
+unused values before register allocation -- and all three round-4 wrong builds (kx6, latec, the N = 6
+batched-squares build) are loads of this kind.  Relaxed long branches (s_getpc / s_add / s_addc /
+s_setpc, emitted in kernels past 128 KB of code) are CFG edges (isa_exec_check.long_branch): until round
+6 they were not, and the N = 9 / 10 objects showed 33 / 14 "arithmetic copied and lost" results -- the
+out-of-bounds restart's new positions, computed in a cold block at the kernel's end that returns by a
+long branch -- which were false findings (every leaf is bit-exact on the GPU,
+tests/test_gpu_v1_parity.py test_out_of_bounds_every_pick); with the edges there are none, and computed
+values gate too.
 
 usage: python scripts/isa_liveness.py [--json] [--all] [--arch=gfx950] <object.o | code-object> ...   (exit 1 on findings)
+       (without --all: loaded values only)
        check_object(path, arch) -> [(kernel, address, instruction [pattern])]
 """
 import os
@@ -284,12 +288,27 @@ def exec_regions(ins, succ):
     return sorted(edges)
 
 
+def long_branch_target(ins, i):
+    """target address of the relaxed long branch ending at ins[i] (isa_exec_check.long_branch), or None"""
+    lb = X.long_branch(ins, i)
+    return None if lb is None else lb[0]
+
+
 def _cfg(ins, lanes=True):
     n = len(ins)
     idx = {a: i for i, (a, _) in enumerate(ins)}
     succ = [[] for _ in range(n)]
     for i, (a, t) in enumerate(ins):
         mn = t.split()[0]
+        if mn == "s_setpc_b64":
+            # a relaxed long branch (kernels past 128 KB of code): without this edge every value that
+            # flows through one looks dead -- the source of the non-gating "arithmetic copied and lost"
+            # findings of round 5 (N = 9 / 10: the out-of-bounds restart block sits at the end of the
+            # kernel and returns to the main body by a long branch)
+            tgt = long_branch_target(ins, i)
+            if tgt is not None and tgt in idx:
+                succ[i].append(idx[tgt])
+            continue
         if mn.startswith(("s_branch", "s_cbranch")):
             off = int(t.split()[1])
             tgt = a + 4 + 4 * (off - 65536 if off >= 32768 else off)
@@ -297,7 +316,7 @@ def _cfg(ins, lanes=True):
                 succ[i].append(idx[tgt])
             if mn.startswith("s_cbranch") and i + 1 < n:
                 succ[i].append(i + 1)
-        elif mn in ("s_endpgm", "s_setpc_b64", "s_trap"):
+        elif mn in ("s_endpgm", "s_trap"):
             pass
         elif i + 1 < n:
             succ[i].append(i + 1)

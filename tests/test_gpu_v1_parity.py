@@ -327,3 +327,94 @@ def test_reset_with_large_v_bias(n, B):
         assert np.array_equal(rew.cpu().numpy().view(np.uint64), r2.view(np.uint64))
         _compare_state(venv, ora, n, B, "after reset step %d" % t)
     venv.close()
+
+
+def _out_of_bounds_states(n, B, seed):
+    """Oracle envs with the ball touching one of the six wall segments (envs_v1/futbol_env.py:247-287:
+    walls 0/1 left, 2 top, 3/4 right, 5 bottom; every 8th env in a corner, where two walls hit and the
+    first in order wins), every player at least 4 from the ball (no touch: the action phase leaves the
+    ball where it is), random owner and RNG event, so that the restart's random.choice picks every
+    player of both teams"""
+    rng = np.random.default_rng(seed)
+    ora = O.V1Vec(B, N=n, seed=seed, portable=True)
+    nb = 2 * n + 1
+    ball = nb - 1
+    corners = [(0.5, 0.5), (0.5, 67.5), (104.5, 0.5), (104.5, 67.5)]
+    for i in range(B):
+        e = ora.envs[i]
+        w = i % 6
+        if i % 8 == 7:
+            bx, by = corners[(i // 8) % 4]
+        elif w in (0, 3):
+            bx, by = (0.5 if w == 0 else 104.5) + rng.uniform(-0.4, 0.4), rng.uniform(2, 22)
+        elif w in (1, 4):
+            bx, by = (0.5 if w == 1 else 104.5) + rng.uniform(-0.4, 0.4), rng.uniform(46, 66)
+        else:
+            bx, by = rng.uniform(5, 100), (67.5 if w == 2 else 0.5) + rng.uniform(-0.4, 0.4)
+        e.px[ball], e.py[ball] = bx, by
+        e.vx[ball], e.vy[ball] = rng.normal(0, 3, 2)
+        for k in range(nb - 1):
+            while True:
+                x, y = rng.uniform(4, 101), rng.uniform(4, 64)
+                if (x - bx) ** 2 + (y - by) ** 2 > 16:
+                    break
+            e.px[k], e.py[k] = x, y
+            e.vx[k], e.vy[k] = rng.normal(0, 3, 2)
+            e.bx[k] = e.by[k] = 0.0
+        e.stamp = 50
+        e.curr_dt = 0.1
+        e.owner = int(rng.integers(0, 2))
+        e.event = int(rng.integers(0, 1 << 20))
+    return ora
+
+
+@pytest.mark.parametrize("rollout", [0, 1])
+@pytest.mark.parametrize("generic", [0, 1])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32], ids=["f64", "f32"])
+@pytest.mark.parametrize("n", [9, 10])
+def test_out_of_bounds_every_pick(n, dtype, generic, rollout, monkeypatch):
+    """Every leaf of the out-of-bounds restart (check_and_fix_out_bounds, envs_v1/futbol_env.py:256-287:
+    the new owner team's random.choice places player `pick` at the ball + (+-1, 0) / (0, +-1)) on every
+    compiled step-kernel instance of N = 9 and 10 (f64 / f32 outputs x default / runtime geometry x
+    step / rollout): the kernels compute that player's new position in each leaf of a switch over
+    `pick`, where the ISA listing shows register copies that are never read.
+    Teacher-forced states put the ball on each wall; the oracle reports the wall and the pick of each
+    env, and every (wall, pick) pair of both teams must occur; obs / reward / done and the full state
+    are compared bit for bit after the restart step and two more."""
+    monkeypatch.setenv("FUTBOL_GENERIC", "1" if generic else "0")
+    B = 2048
+    seed = 700 + n
+    ora = _out_of_bounds_states(n, B, seed)
+    venv = _venv(n, B, seed, dtype)
+    venv.set_state(v1_oracle_to_state(ora.envs, n, B))
+    v1_state_to_oracle(venv.get_state(), ora.envs, n, B)
+    a = torch.zeros((3, B, 2 * n), dtype=torch.uint8, device=venv.device)  # left team: noop
+    a[1:] = venv.random_actions_steps(2, 1, seed=55)
+    a_np = a.cpu().numpy().astype(np.int32)
+    if rollout:
+        obs, rew, done, _ = venv.rollout(a)
+        outs = [(obs[t].cpu().numpy(), rew[t].cpu().numpy(), done[t].cpu().numpy()) for t in range(3)]
+    else:
+        outs = []
+        for t in range(3):
+            o, r, d, _ = venv.step(a[t])
+            outs.append((o.cpu().numpy(), r.cpu().numpy(), d.cpu().numpy()))
+    seen = set()
+    cast = np.float32 if dtype == torch.float32 else np.float64
+    ut = np.uint32 if dtype == torch.float32 else np.uint64
+    for t in range(3):
+        o2, r2, d2, _ = ora.step(a_np[t])
+        if t == 0:
+            for e in ora.envs:
+                assert e.last_out_wall >= 0, "every env must restart from out of bounds on the first step"
+                seen.add((int(e.last_out_wall), int(e.last_out_pick)))
+        o1, r1, d1 = outs[t]
+        assert np.array_equal(d1.astype(bool), d2), "done, step %d" % t
+        assert np.array_equal(r1.view(ut), r2.astype(cast).view(ut)), "reward, step %d" % t
+        bad = ~(o1.view(ut) == o2.astype(cast).view(ut)).all(axis=1)
+        assert not bad.any(), "obs of env %d at step %d (wall %d)" % (int(np.flatnonzero(bad)[0]), t,
+                                                                        ora.envs[int(np.flatnonzero(bad)[0])].last_out_wall)
+    _compare_state(venv, ora, n, B, "out of bounds, 3 steps")
+    missing = {(w, p) for w in range(6) for p in range(2 * n)} - seen
+    assert not missing, "uncovered (wall, pick) leaves: %s" % sorted(missing)[:10]
+    venv.close()

@@ -56,15 +56,16 @@ def _kernel(lines, base=0x1000):
 @pytest.mark.skipif(not OBJS or not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-objdump"),
                     reason="no built objects / ROCm LLVM tools")
 def test_no_lost_loads_in_shipped_objects():
-    """No loaded value of the shipped kernels is only copied into registers nobody reads (the round-4
-    kx6 / latec faults).  One child process per object, as the build gate runs it."""
+    """No loaded or computed value of the shipped kernels is only copied into registers nobody reads (the
+    round-4 kx6 / latec / N = 6 faults).  One child process per object, as the build
+    gate runs it (--all: computed values too, since round 6)."""
     import json
     import subprocess
     from concurrent.futures import ThreadPoolExecutor
     tool = os.path.join(ROOT, "scripts", "isa_liveness.py")
 
     def one(o):
-        r = subprocess.run([sys.executable, tool, "--json", o], capture_output=True, text=True)
+        r = subprocess.run([sys.executable, tool, "--json", "--all", o], capture_output=True, text=True)
         assert r.returncode in (0, 1), r.stderr[-2000:]
         return [(os.path.basename(o),) + tuple(f) for f in json.loads(r.stdout.splitlines()[0])["findings"]]
     with ThreadPoolExecutor(min(8, os.cpu_count() or 4)) as ex:
@@ -117,3 +118,50 @@ def test_exec_scanner_limits_are_measured():
     assert len(I.scan(_kernel(at_join))) == 1
     fallthrough = [t for t in at_join if not t.startswith("s_cbranch")]
     assert I.scan(_kernel(fallthrough)) == []
+
+
+def _long_jump(from_index, to_index, sreg=98, base=0x1000):
+    """the four instructions of a relaxed long branch placed at index from_index (its s_getpc) to index
+    to_index: s_getpc_b64; s_add_u32 lo; s_addc_u32 hi; s_setpc_b64 (LLVM's branch relaxation)"""
+    off = (base + 4 * to_index) - (base + 4 * from_index + 4)
+    lo, hi = off & 0xffffffff, (off >> 32) & 0xffffffff
+    s = "s[%d:%d]" % (sreg, sreg + 1)
+    return ["s_getpc_b64 " + s, "s_add_u32 s%d, s%d, 0x%x" % (sreg, sreg, lo),
+            "s_addc_u32 s%d, s%d, %s" % (sreg + 1, sreg + 1, "-1" if hi == 0xffffffff else "0x%x" % hi),
+            "s_setpc_b64 " + s]
+
+
+def test_liveness_follows_relaxed_long_branches():
+    """Round 6: kernels past 128 KB of code (N >= 8) leave a cold block at the end and return from it by a
+    relaxed long branch (s_getpc / s_add / s_addc / s_setpc).  The liveness CFG follows it: a value computed
+    in the cold block and used after the jump back is live.  Without that edge the N = 9 / 10 objects
+    showed 33 / 14 "arithmetic copied and lost" results (the out-of-bounds restart's new positions) --
+    false findings, since every leaf of that switch is bit-exact on the GPU (test_gpu_v1_parity.py
+    test_out_of_bounds_every_pick)."""
+    import isa_liveness as L
+    # 0: branch to the cold block; 1-2: main body after the return point (index 1 uses a4)
+    main = ["s_branch 3", "global_store_dword v[8:9], v4, off", "s_endpgm"]
+    # 3..: cold block: computes v[2:3], copies to a4, jumps back to index 1
+    cold = ["global_load_dwordx2 v[2:3], v10, s[0:1]", "s_waitcnt vmcnt(0)", "v_accvgpr_write_b32 a4, v2",
+            "v_accvgpr_read_b32 v4, a4"]
+    lst = main + cold + _long_jump(len(main) + len(cold), 1)
+    assert L.scan(_kernel(lst)) == [], "the value reaches the store through the long branch"
+    # the same listing with an unresolvable setpc (a computed target) drops the edge: the value is lost
+    broken = main + cold + ["s_setpc_b64 s[30:31]"]
+    assert len(L.scan(_kernel(broken))) == 1
+
+
+def test_exec_scanner_checks_relaxed_execz_joins():
+    """A relaxed s_cbranch_execz (s_cbranch_execnz over a long branch): the long branch's target is a join
+    entered with exec = 0 when taken, so a copy placed there before the exec restore is the round-3 fault
+    pattern -- the scanner must see it."""
+    import isa_exec_check as I
+    head = ["s_and_saveexec_b64 s[4:5], vcc", "s_cbranch_execnz 4"]
+    jump_at = len(head)
+    body = ["v_add_u32_e32 v1, v1, v2", "s_endpgm"]
+    join = ["v_accvgpr_write_b32 a144, v232", "s_or_b64 exec, exec, s[4:5]", "s_endpgm"]
+    join_at = jump_at + 4 + len(body)
+    lst = head + _long_jump(jump_at, join_at) + body + join
+    f = I.scan(_kernel(lst))
+    assert len(f) == 1 and f[0][1] == hex(0x1000 + 4 * join_at), f
+    assert I.scan(_kernel(lst[:join_at] + join[1:])) == []
