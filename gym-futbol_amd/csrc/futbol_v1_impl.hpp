@@ -324,6 +324,22 @@ __device__ __forceinline__ T& soa(T* base, int k, int B, int env)
     return *reinterpret_cast<T*>(reinterpret_cast<char*>(base + (size_t)k * (size_t)B) + (uint32_t)env * (uint32_t)sizeof(T));
 }
 
+// The step's final stores address every row again through a copy of the lane's env index that the
+// compiler cannot see through (an empty asm): otherwise it reuses the 64-bit row addresses computed for
+// the step's loads, and keeps them -- 2 VGPRs per row and field, from the loads at the top to the stores
+// at the end -- live through the whole step (N >= 6: spilled to scratch).  Recomputed at the stores they
+// are one add each (FUTBOL_OPAQUE_MIN, round 6)
+#ifndef FUTBOL_OPAQUE_MIN
+#define FUTBOL_OPAQUE_MIN 99
+#endif
+template <int N>
+constexpr bool kOpaqueStore = N >= FUTBOL_OPAQUE_MIN;
+__device__ __forceinline__ int opaque_lane(int x)
+{
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
 // global spill record (slot s >= K): 8 doubles [nx, ny, nMass, info, bias, -bounce, jBias, jnAcc]
 // (the LDS record's four double2 in order), at spill[env][s - K][f]: a record is one 64-byte line,
 // so the solve's per-sweep re-reads of an item's spill records stay in a few cache lines
@@ -585,7 +601,9 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
     const double damping = dtc == 2 ? P.damp[2] : P.damp[1];
     const double slop = P.slop, W = P.W, H = P.H;
     e.meta.set_dtcode(dtc);
-    const int B = L.B, env = L.env;
+    // (kOpaqueStore: the env index through an empty asm, so that the arbiter-cache and spill-record
+    // addresses of this cpSpaceStep are computed here, not reused from the step's first loads)
+    const int B = L.B, env = kOpaqueStore<N> ? opaque_lane(L.env) : L.env;
     uint32_t ncache = e.meta.ncache();
     FB_BOUND(L, ncache <= (uint32_t)S::P, 1, ncache = S::P);
 
@@ -1757,8 +1775,9 @@ __device__ __forceinline__ void load_env(const V1Ptrs& st, int env, int B, Env<N
 }
 
 template <int N>
-__device__ __forceinline__ void store_env(const V1Ptrs& st, int env, int B, const Env<N>& e)
+__device__ __forceinline__ void store_env(const V1Ptrs& st, int env_, int B, const Env<N>& e)
 {
+    const int env = kOpaqueStore<N> ? opaque_lane(env_) : env_;
     if constexpr (kScalarBase<N>) {
         sfor<V1Shape<N>::Nb>([&](auto K) {
             constexpr int k = K;
@@ -2293,16 +2312,17 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
         FUTBOL_STAMP(ph == 0 ? 8 : 9);
     }
     FUTBOL_CRUMB(L, 80);
+    const int eo = kOpaqueStore<N> ? opaque_lane(env) : env;  // (the step's output addresses, computed here)
     if constexpr (kScalarBase<N>) {
-        write_obs<N, OT>(e, obs + (size_t)((uint32_t)env * (uint32_t)(4 * S::Nb)));
-        soa(st.ep_ret, 0, B, env) = ret;
-        soa(reward, 0, B, env) = (OT)r;
-        soa(done_out, 0, B, env) = done ? 1 : 0;
+        write_obs<N, OT>(e, obs + (size_t)((uint32_t)eo * (uint32_t)(4 * S::Nb)));
+        soa(st.ep_ret, 0, B, eo) = ret;
+        soa(reward, 0, B, eo) = (OT)r;
+        soa(done_out, 0, B, eo) = done ? 1 : 0;
     } else {
-    write_obs<N, OT>(e, obs + (size_t)env * (4 * S::Nb));
-    st.ep_ret[env] = ret;
-    reward[env] = (OT)r;
-    done_out[env] = done ? 1 : 0;
+    write_obs<N, OT>(e, obs + (size_t)eo * (4 * S::Nb));
+    st.ep_ret[eo] = ret;
+    reward[eo] = (OT)r;
+    done_out[eo] = done ? 1 : 0;
     }
     store_env<N>(st, env, B, e);
     // The clamped-action count (futbol_invalid_actions) is the step's last memory operation, where no
