@@ -328,9 +328,11 @@ __device__ __forceinline__ T& soa(T* base, int k, int B, int env)
 // compiler cannot see through (an empty asm): otherwise it reuses the 64-bit row addresses computed for
 // the step's loads, and keeps them -- 2 VGPRs per row and field, from the loads at the top to the stores
 // at the end -- live through the whole step (N >= 6: spilled to scratch).  Recomputed at the stores they
-// are one add each (FUTBOL_OPAQUE_MIN, round 6)
+// are one add each (FUTBOL_OPAQUE_MIN, round 6).  Measured (profiles/r06/ab/c2/, two runs each): 10v10
+// 137.4 -> 129.7 us (scratch 664 -> 400 B per lane), 9v9 113.5 -> 106.6, 8v8 100.9 -> 96.8; 6v6 and 5v5
+// equal, 2v2 22.15 -> 22.48 (+1.5%), 7v7 slower (its build needed the ISA gate's max-ilp fallback): N >= 8
 #ifndef FUTBOL_OPAQUE_MIN
-#define FUTBOL_OPAQUE_MIN 99
+#define FUTBOL_OPAQUE_MIN 8
 #endif
 template <int N>
 constexpr bool kOpaqueStore = N >= FUTBOL_OPAQUE_MIN;
