@@ -423,7 +423,14 @@ def suspects(ins, loads_only=True):
             continue
         live = [bool(strong[i] & _bit(r)) for r in rs]
         read = [bool(weak[i] & _bit(r)) for r in rs]
-        if any((not l) and w for l, w in zip(live, read)):
+        lost = any((not l) and w for l, w in zip(live, read))
+        if lost and not LOADS.match(t) and any(live):
+            # a computed multi-register value whose used part is live: a 64-bit operation of which only one
+            # half is needed (v_lshrrev_b64 for a 32-bit result) moved as a pair -- the other half's copy is
+            # dead by construction, not a misplaced copy.  Loads are judged per register (the kx6 / N = 6
+            # faults: one dword of a 16-byte load lost while the others are used)
+            lost = False
+        if lost:
             out.append((i, "".join("L" if l else ("c" if w else ".") for l, w in zip(live, read))))
     return out
 

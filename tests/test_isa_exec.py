@@ -165,3 +165,19 @@ def test_exec_scanner_checks_relaxed_execz_joins():
     f = I.scan(_kernel(lst))
     assert len(f) == 1 and f[0][1] == hex(0x1000 + 4 * join_at), f
     assert I.scan(_kernel(lst[:join_at] + join[1:])) == []
+
+
+def test_liveness_partial_use_of_computed_pairs():
+    """--all judges computed values whole: a 64-bit shift whose high half is unused but moved with the pair
+    (v_mov_b64) is not a finding, a computed pair lost entirely is -- and a load is judged per register."""
+    import isa_liveness as L
+    part = ["v_lshrrev_b64 v[6:7], v2, v[8:9]", "v_mov_b64_e32 v[10:11], v[6:7]",
+            "global_store_dword v[20:21], v10, off", "s_endpgm"]
+    assert L.scan(_kernel(part), loads_only=False) == []
+    whole = ["v_add_f64 v[6:7], v[2:3], v[4:5]", "v_mov_b64_e32 v[10:11], v[6:7]", "s_endpgm"]
+    f = L.scan(_kernel(whole), loads_only=False)
+    assert len(f) == 1 and f[0][2].endswith("[cc]"), f
+    load = ["global_load_dwordx2 v[6:7], v2, s[0:1]", "s_waitcnt vmcnt(0)", "v_mov_b64_e32 v[10:11], v[6:7]",
+            "global_store_dword v[20:21], v10, off", "s_endpgm"]
+    f = L.scan(_kernel(load))
+    assert len(f) == 1 and f[0][2].endswith("[Lc]"), f
