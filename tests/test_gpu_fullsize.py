@@ -1,7 +1,8 @@
 """The benchmark's workload at its full size, on the GPU, EVERY env compared with the oracle at
 every step: B = 65 536 envs per context (1 024 one-wave blocks: one wave per SIMD, every XCD),
 float32 outputs (the bench's kernel instance), synthetic device actions, auto-reset across an
-episode boundary -- C2 (2v2), C5 (5v5) and C3 (v0, hard-coded opponent).
+episode boundary -- C2 (2v2), C5 (5v5) and C3 (v0, hard-coded opponent); 10v10 (`Futbol-v1`) for 80
+steps; and the open-loop rollout instance of 2v2 / 5v5 (two 30-step launches).
 
 The portable oracle steps the same 65 536 global env ids beside the kernel (OpenMP over the box's
 CPU share, ~10 s of oracle per config), and obs / reward / done (and the terminal observations of
@@ -69,6 +70,36 @@ def _check(kind, n, T, period):
 @pytest.mark.parametrize("n", [2, 5])
 def test_v1_full_size_every_env(n):
     _check("v1", n, 320, 300)
+
+
+def test_v1_10v10_full_size_every_env():
+    """Futbol-v1 (N = 10, SURVEY 8(f) #3) at the same 65 536 envs: 80 steps (its oracle is ~5x the 5v5 one)"""
+    _check("v1", 10, 80, 300)
+
+
+@pytest.mark.parametrize("n", [2, 5])
+def test_v1_full_size_rollout_every_env(n):
+    """The open-loop rollout instance (bench.py's open_loop_rollout companion line) at the full size: 2
+    launches of 30 steps, every env's obs / reward / done of every step against the oracle"""
+    from gym_futbol_amd import FutbolVecEnv
+    seed = 41 + n
+    venv = FutbolVecEnv("v1", B, seed=seed, dtype=torch.float32, number_of_player=n)
+    ora = O.V1Vec(B, N=n, seed=seed, portable=True)
+    o = venv.reset().cpu().numpy()
+    assert np.array_equal(o.view(np.uint32), ora.reset().astype(np.float32).view(np.uint32))
+    K = 30
+    for c in range(2):
+        acts = venv.random_actions_steps(K, c * K, seed=99)
+        obs, rew, done, _ = venv.rollout(acts)
+        a_np = acts.cpu().numpy().astype(np.int32)
+        o1, r1, d1 = obs.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy().astype(bool)
+        for t in range(K):
+            o2, r2, d2, _ = ora.step(a_np[t], nthreads=NT)
+            eq = (d1[t] == d2) & (r1[t].view(np.uint32) == r2.astype(np.float32).view(np.uint32))
+            eq &= (o1[t].reshape(B, -1).view(np.uint32) == o2.reshape(B, -1).astype(np.float32).view(np.uint32)).all(axis=1)
+            i = _first_bad(eq)
+            assert i is None, "rollout N=%d: env %d differs at step %d" % (n, i, c * K + t)
+    venv.close()
 
 
 def test_v0_full_size_every_env():
