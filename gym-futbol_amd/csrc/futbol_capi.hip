@@ -206,6 +206,15 @@ extern "C" int futbol_create(const FutbolConfig* cfg, int32_t device, uint64_t s
         return fail(nullptr, FUTBOL_EUNSUPPORTED, "number_of_player must be 1..10 (team.py:52-112)");
     if (cfg->env_kind != FUTBOL_ENV_V1 && cfg->env_kind != FUTBOL_ENV_V0)
         return fail(nullptr, FUTBOL_EINVAL, "env_kind");
+    if (cfg->env_kind == FUTBOL_ENV_V1) {
+        // the N >= 6 step instances address per-env data as a wave-uniform row base plus a 32-bit lane
+        // offset (kScalarBase, futbol_v1_impl.hpp): env * 16 bytes (a double2 row element) and the
+        // observation element offset env * 4 Nb must fit 32 bits.  Unreachable in practice (10v10 needs
+        // ~51 M envs, whose spill area alone exceeds the HBM) -- checked for every N all the same
+        const uint64_t nb = 2u * (uint64_t)cfg->number_of_player + 1u;
+        if ((uint64_t)num_envs * 16u >= (1ull << 32) || (uint64_t)num_envs * 4u * nb >= (1ull << 32))
+            return fail(nullptr, FUTBOL_EINVAL, "num_envs too large for the kernels' 32-bit per-env offsets");
+    }
 
     FutbolCtx* ctx = new FutbolCtx();
     ctx->cfg = *cfg;
@@ -227,14 +236,6 @@ extern "C" int futbol_create(const FutbolConfig* cfg, int32_t device, uint64_t s
     };
     if (cfg->env_kind == FUTBOL_ENV_V1) {
         const int N = cfg->number_of_player, Nb = 2 * N + 1, P = v1_npairs(N);
-        // the N >= 6 step instances address per-env data as a wave-uniform row base plus a 32-bit lane
-        // offset (kScalarBase, futbol_v1_impl.hpp): env * 16 bytes (a double2 row element) and the
-        // observation element offset env * 4 Nb must fit 32 bits.  Unreachable in practice (10v10 needs
-        // ~51 M envs, whose spill area alone exceeds the HBM) -- checked for every N all the same
-        if ((uint64_t)B * 16u >= (1ull << 32) || (uint64_t)B * 4u * (uint64_t)Nb >= (1ull << 32)) {
-            delete ctx;
-            return fail(nullptr, FUTBOL_EINVAL, "num_envs too large for the kernels' 32-bit per-env offsets");
-        }
         ctx->N = N;
         ctx->obs_dim = 4 * Nb;
         ctx->act_dim = 2 * N;

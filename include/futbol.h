@@ -76,7 +76,9 @@ typedef struct FutbolCtx FutbolCtx;
 int futbol_config_default(int32_t env_kind, int32_t number_of_player, FutbolConfig* cfg);
 
 /* Create B envs on `device`; env i has global id env_id_base + i (RNG key).
-   Runs each env's constructor (which in the reference already calls reset()). */
+   Runs each env's constructor (which in the reference already calls reset()).
+   FUTBOL_EINVAL if env_id_base + B exceeds 32 bits, or if B * 16 or B * obs_dim does not fit 32 bits
+   (the kernels' per-env offsets; no GPU memory holds that many envs anyway). */
 int futbol_create(const FutbolConfig* cfg, int32_t device, uint64_t seed, uint64_t env_id_base,
                   int32_t num_envs, FutbolCtx** out);
 /* Releases every resource of ctx (NULL: no-op) whatever fails; returns FUTBOL_EHIP if a HIP call

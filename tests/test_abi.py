@@ -73,6 +73,9 @@ def test_create_rejects_bad_arguments_without_touching_a_device(nat):
     assert lib.futbol_create(C.byref(cfg), 0, 0, 0, 8, C.byref(h)) == -1
     cfg = nat.default_config(nat.ENV_V1, 2)
     assert lib.futbol_create(C.byref(cfg), 0, 0, 2**32 - 4, 8, C.byref(h)) == -1  # env ids > 32 bits
+    cfg = nat.default_config(nat.ENV_V1, 10)                                      # 32-bit per-env offsets
+    assert lib.futbol_create(C.byref(cfg), 0, 0, 0, 60_000_000, C.byref(h)) == -1
+    assert b"32-bit" in lib.futbol_last_error(None)
     assert lib.futbol_step(None, None, None, None, None, None, None) == -1
 
 
