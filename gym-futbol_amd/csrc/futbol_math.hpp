@@ -478,7 +478,42 @@ __device__ __forceinline__ void glibc_pow2_need_lds(const double (&x)[M], double
 // max-over-lanes(pending) rounds; up to 64 squares.
 template <int M>
 __host__ __device__ __forceinline__ void glibc_pow2_need(const double (&x)[M], double (&h)[M], uint64_t need,
-                                                        const double* logt = kPowLog, const uint64_t* expt = kPowExp)
+                                                        const double* logt = kPowLog, const uint64_t* expt = kPowExp);
+// glibc_pow2_full as a real call (global-memory tables): the envs_v1 instances at the register limit inline
+// it at every player and body (~40 copies for 10v10), and the compiler hoists the copies' polynomial
+// constants out of them -- materialised once, then spilled to scratch for the whole step
+__host__ __device__ __attribute__((noinline)) inline double glibc_pow2_full_call(double x)
+{
+    return glibc_pow2_full(x);
+}
+template <int M, bool CALL>
+__host__ __device__ __forceinline__ void glibc_pow2_need_t(const double (&x)[M], double (&h)[M], uint64_t need)
+{
+    static_assert(M <= 64, "pending mask");
+    uint64_t pend = 0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+        h[i] = x[i] * x[i];
+        pend |= (uint64_t)pow2_near_midpoint(h[i], fma(x[i], x[i], -h[i])) << i;
+    }
+    pend &= need;
+#ifdef FUTBOL_DIAG_PLAIN_SQ  // diagnostic builds only (cost of the exact squares): x*x, NOT glibc's
+    pend = 0u;
+#endif
+    while (__builtin_expect(pend != 0u, 0)) {
+        const uint64_t bit = pend & (0ull - pend);
+        double v = 0.0;
+#pragma unroll
+        for (int i = 0; i < M; ++i) v = bit == (1ull << i) ? x[i] : v;
+        const double f = CALL ? glibc_pow2_full_call(v) : glibc_pow2_full(v);
+#pragma unroll
+        for (int i = 0; i < M; ++i) h[i] = bit == (1ull << i) ? f : h[i];
+        pend &= pend - 1u;
+    }
+}
+template <int M>
+__host__ __device__ __forceinline__ void glibc_pow2_need(const double (&x)[M], double (&h)[M], uint64_t need,
+                                                        const double* logt, const uint64_t* expt)
 {
     static_assert(M <= 64, "pending mask");
     uint64_t pend = 0;

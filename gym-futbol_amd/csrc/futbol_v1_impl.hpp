@@ -94,6 +94,12 @@ constexpr int KXN = N == 5 ? FUTBOL_SPILL_REGS : (N >= 6 ? FUTBOL_SPILL_REGS_BIG
 #endif
 template <int N>
 constexpr bool kSqBatch = N <= FUTBOL_SQ_BATCH_MAX;
+// (N >= FUTBOL_POW_CALL_MIN: the per-body glibc squares' slow path as a call, glibc_pow2_full_call)
+#ifndef FUTBOL_POW_CALL_MIN
+#define FUTBOL_POW_CALL_MIN 99
+#endif
+template <int N>
+constexpr bool kPowCall = N >= FUTBOL_POW_CALL_MIN;
 
 // Diagnostic build only (-DFUTBOL_STAMPS, bench.py --stamps): per-wave s_memtime at phase
 // boundaries, accumulated into st.stamps[wave][slot] (kStampStride slots per wave: 0-10 phases,
@@ -1183,7 +1189,7 @@ __device__ __forceinline__ void space_step(const V1Params& P, const Lane<N, EPW>
             const bool near = e.vx[k] * e.vx[k] + e.vy[k] * e.vy[k] > thr * (1.0 - 0x1.0p-40);
             const double vq[2] = {e.vx[k], e.vy[k]};
             double vsq[2];
-            glibc_pow2_need<2>(vq, vsq, near ? 3ull : 0ull);
+            glibc_pow2_need_t<2, kPowCall<N>>(vq, vsq, near ? 3ull : 0ull);
             const double s2 = vsq[0] + vsq[1];
             if (near && s2 > thr) {
                 constexpr double vmax = k == S::BALL ? kBallVmax : kPlayerVmax;
@@ -2168,7 +2174,7 @@ __device__ __forceinline__ void v1_step_body(const V1Params& P, const V1Params* 
         } else {  // N >= 6: this player's two squares (tables from global memory)
             const double q2[2] = {dx, dy};
             double s2[2];
-            glibc_pow2_need<2>(q2, s2, (press | shoot | pass) ? 3ull : 0ull);
+            glibc_pow2_need_t<2, kPowCall<N>>(q2, s2, (press | shoot | pass) ? 3ull : 0ull);
             sx = s2[0];
             sy = s2[1];
             (void)tsx;

@@ -92,6 +92,10 @@ def defs_uses(text):
         if re.search(r"\b(sc0|glc)\b", rest):
             return regs(ops[0]), [r for o in ops[1:] for r in regs(o)]
         return [], [r for o in ops for r in regs(o)]
+    if mn == "s_swappc_b64":
+        # a call (a device function, e.g. glibc_pow2_full_call): its arguments are v0-v31 under the AMDGPU
+        # calling convention; counted as read (conservative: nothing the caller passes looks lost)
+        return [], [("v", r) for r in range(32)]
     if not ops:
         return [], []
     d = regs(ops[0])
@@ -298,6 +302,7 @@ def _cfg(ins, lanes=True):
     n = len(ins)
     idx = {a: i for i, (a, _) in enumerate(ins)}
     succ = [[] for _ in range(n)]
+    rets = set()
     for i, (a, t) in enumerate(ins):
         mn = t.split()[0]
         if mn == "s_setpc_b64":
@@ -308,6 +313,8 @@ def _cfg(ins, lanes=True):
             tgt = long_branch_target(ins, i)
             if tgt is not None and tgt in idx:
                 succ[i].append(idx[tgt])
+            else:
+                rets.add(i)  # a device function's return: every register counts as live out
             continue
         if mn.startswith(("s_branch", "s_cbranch")):
             off = int(t.split()[1])
@@ -338,6 +345,7 @@ def _cfg(ins, lanes=True):
     bend = {}
     for k, s in enumerate(starts):
         bend[s] = (starts[k + 1] if k + 1 < len(starts) else n) - 1
+    _cfg.rets = {s for s in starts if bend[s] in rets}
     return starts, bend, {s: list(succ[bend[s]]) for s in starts}
 
 
@@ -365,12 +373,14 @@ def liveness(ins, strong=False, lanes=True):
                     add |= _bit(u)
             return (live & ~dmask[i]) | add
         return (live & ~dmask[i]) | umask[i]
+    rets = _cfg.rets
+    ALL = (1 << 1024) - 1
     live_in = {s: 0 for s in starts}
     changed = True
     while changed:
         changed = False
         for s in reversed(starts):
-            live = 0
+            live = ALL if s in rets else 0
             for t in bsucc[s]:
                 live |= live_in[t]
             for i in range(bend[s], s - 1, -1):
@@ -380,7 +390,7 @@ def liveness(ins, strong=False, lanes=True):
                 changed = True
     after = [0] * n
     for s in starts:
-        live = 0
+        live = ALL if s in rets else 0
         for t in bsucc[s]:
             live |= live_in[t]
         for i in range(bend[s], s - 1, -1):

@@ -146,8 +146,9 @@ def test_liveness_follows_relaxed_long_branches():
             "v_accvgpr_read_b32 v4, a4"]
     lst = main + cold + _long_jump(len(main) + len(cold), 1)
     assert L.scan(_kernel(lst)) == [], "the value reaches the store through the long branch"
-    # the same listing with an unresolvable setpc (a computed target) drops the edge: the value is lost
-    broken = main + cold + ["s_setpc_b64 s[30:31]"]
+    # without the jump back (the cold block ending the program) the same value is lost -- the finding the
+    # long branch's edge removes (an undecodable s_setpc is a function return: everything live, no finding)
+    broken = main + cold + ["s_endpgm"]
     assert len(L.scan(_kernel(broken))) == 1
 
 
@@ -181,3 +182,15 @@ def test_liveness_partial_use_of_computed_pairs():
             "global_store_dword v[20:21], v10, off", "s_endpgm"]
     f = L.scan(_kernel(load))
     assert len(f) == 1 and f[0][2].endswith("[Lc]"), f
+
+
+def test_liveness_models_calls_and_returns():
+    """A device function's return (s_setpc_b64 of its return address, not a decodable long branch) leaves every
+    register live -- its result in v[0:1] is not lost -- and a call (s_swappc_b64) reads the argument registers
+    v0-v31, so the value the caller passes is not lost either (round 6: glibc_pow2_full_call)."""
+    import isa_liveness as L
+    callee = ["v_mul_f64 v[2:3], v[0:1], v[0:1]", "v_mov_b64_e32 v[0:1], v[2:3]", "s_setpc_b64 s[30:31]"]
+    assert L.scan(_kernel(callee), loads_only=False) == []
+    caller = ["global_load_dwordx2 v[6:7], v10, s[0:1]", "s_waitcnt vmcnt(0)", "v_mov_b64_e32 v[0:1], v[6:7]",
+              "s_swappc_b64 s[30:31], s[16:17]", "global_store_dwordx2 v[20:21], v[0:1], off", "s_endpgm"]
+    assert L.scan(_kernel(caller)) == []
