@@ -342,6 +342,11 @@ __device__ __forceinline__ T& soa(T* base, int k, int B, int env)
 #endif
 template <int N>
 constexpr bool kOpaqueStore = N >= FUTBOL_OPAQUE_MIN;
+#ifndef FUTBOL_OPAQUE_PRE_MIN
+#define FUTBOL_OPAQUE_PRE_MIN 99
+#endif
+template <int N>
+constexpr bool kOpaquePre = N >= FUTBOL_OPAQUE_PRE_MIN;
 __device__ __forceinline__ int opaque_lane(int x)
 {
     asm volatile("" : "+v"(x));
@@ -575,11 +580,14 @@ __device__ __forceinline__ void load_cache_pre(const Lane<N, EPW>& L, uint32_t n
                                                double (&cj)[CKN<N>])
 {
     static_assert(CKN<N> <= V1Shape<N>::P, "preloaded cache entries must lie inside the [P][B] arrays");
+    // (N >= FUTBOL_OPAQUE_PRE_MIN: the addresses computed afresh, not kept from the step's first call for the
+    // restart phases' -- 10v10: 32 B less scratch per lane)
+    const int env = kOpaquePre<N> ? opaque_lane(L.env) : L.env;
 #pragma unroll
     for (int c = 0; c < CKN<N>; ++c) {
         if constexpr (kScalarBase<N>) {
-            const uint32_t k = soa(L.ckey, c, L.B, L.env);
-            const double j = soa(L.cjn, c, L.B, L.env);
+            const uint32_t k = soa(L.ckey, c, L.B, env);
+            const double j = soa(L.cjn, c, L.B, env);
             ck[c] = (uint32_t)c < ncache ? k : 0xffffu;
             cj[c] = (uint32_t)c < ncache ? j : 0.0;
         } else {
