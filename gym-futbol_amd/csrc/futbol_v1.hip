@@ -76,11 +76,15 @@ bool v1_is_default_geometry(int N, const V1Params& p)
 int v1_supported(int N) { return N >= 1 && N <= 10; }
 int v1_supported_epw(int epw) { return epw == 64; }
 
-// spill slots needed in the worst case (largest EPW = fewest LDS slots)
+// spill slots needed in the worst case: the pairs past the LDS record slots of the kernel's OWN
+// translation unit (layout_v1), not this one's V1Shape -- an A/B build of one TU with fewer slots
+// (FUTBOL_K5=3) would otherwise index past the allocation
 size_t v1_spill_slots(int N)
 {
+    int32_t o[8];
+    if (layout_v1(N, o)) return 0;
     switch (N) {
-#define FUTBOL_CASE(n) case n: return V1Shape<n>::P - V1Shape<n>::K;
+#define FUTBOL_CASE(n) case n: return (size_t)(V1Shape<n>::P - (o[0] < V1Shape<n>::P ? o[0] : V1Shape<n>::P));
     FUTBOL_CASE(1) FUTBOL_CASE(2) FUTBOL_CASE(3) FUTBOL_CASE(4) FUTBOL_CASE(5)
     FUTBOL_CASE(6) FUTBOL_CASE(7) FUTBOL_CASE(8) FUTBOL_CASE(9) FUTBOL_CASE(10)
 #undef FUTBOL_CASE

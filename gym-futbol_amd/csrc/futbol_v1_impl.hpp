@@ -2391,8 +2391,13 @@ __global__ void __launch_bounds__(EPW) FUTBOL_V1_STEP_ATTR v1_step_kernel(const 
                                                       OT* __restrict__ term_obs, int nsteps)
 {
     // 4 blocks per CU (160 KB of LDS) up to N = 7 and with one row set, 3 blocks otherwise
+    // (FUTBOL_LDS_BLOCKS_PER_CU: an A/B build that trades blocks per CU for LDS record slots)
+#ifndef FUTBOL_LDS_BLOCKS_PER_CU
     static_assert(sizeof(Scratch<N, EPW>) <= (N <= 7 || V1Shape<N>::ONE_ROWS ? 160 * 1024 / 4 : 160 * 1024 / 3),
                   "LDS per block");
+#else
+    static_assert(sizeof(Scratch<N, EPW>) <= 160 * 1024 / FUTBOL_LDS_BLOCKS_PER_CU, "LDS per block");
+#endif
     __shared__ Scratch<N, EPW> sh;
     using S = V1Shape<N>;
     if constexpr (!ROLL) {
